@@ -1,0 +1,104 @@
+/*
+ * ape_lz4_gpu.h -- batched MI355X LZ4 block codec: the performance path.
+ *
+ * Each entry point runs N *independent* LZ4 blocks on the calling thread's
+ * current HIP device, one workgroup per block.  Per-block results use exactly
+ * the conventions of the single-block calls they batch:
+ *
+ *   APE_LZ4_compress_batch_dev       == N x APE_LZ4_compress_default
+ *                                        (ref src/ape_lz4.c:811-815)
+ *   APE_LZ4_decompress_safe_batch_dev == N x APE_LZ4_decompress_safe
+ *                                        (ref src/ape_lz4.c:1472-1478)
+ *   ..._partial_batch_dev            == N x APE_LZ4_decompress_safe_partial
+ *                                        (ref src/ape_lz4.c:1480-1487)
+ *
+ * Compression emits a valid LZ4 v1.7.1 block (decodable by the reference
+ * decompress_safe with cap = srcSize) but not the reference's byte stream:
+ * the GPU parse is its own.  Decompression is bit-exact
+ * with the reference: same return value, same dst[0:ret].
+ *
+ * Pointers named d_* are device pointers (hipMalloc / torch CUDA tensors).
+ * `stream` is a hipStream_t passed as void* (NULL = default stream).  All
+ * launchers are asynchronous and graph-capturable (no allocation, no sync).
+ * Return value of a launcher: 0 on success, otherwise a negative
+ * APE_LZ4_GPU_E* code (nothing was launched); per-block status is in d_result.
+ *
+ * GPU limits: blocks are at most APE_LZ4_GPU_MAX_BLOCK (65536) bytes on the
+ * uncompressed side (the LZ4 window; the benchmark's 64 KiB block).  A block
+ * whose decoded output would exceed it gets d_result = APE_LZ4_GPU_ERANGE.
+ */
+#pragma once
+#include <stddef.h>
+
+#if defined(__cplusplus)
+extern "C" {
+#endif
+
+#define APE_LZ4_GPU_MAX_BLOCK 65536
+#define APE_LZ4_GPU_ERANGE (-2147483647 - 1) /* per-block: size outside GPU limits */
+
+enum {
+    APE_LZ4_GPU_OK = 0,
+    APE_LZ4_GPU_ENODEV = -1,   /* no usable MI355X / HIP runtime          */
+    APE_LZ4_GPU_EINVAL = -2,   /* bad argument (N < 0, null pointer ...)  */
+    APE_LZ4_GPU_ELAUNCH = -3,  /* kernel launch / HIP runtime error        */
+    APE_LZ4_GPU_ENOMEM = -4    /* staging allocation failed                */
+};
+
+/* Runtime. */
+int APE_LZ4_gpu_init(void);                 /* 0 if a gfx950 device is usable */
+int APE_LZ4_gpu_device_count(void);
+const char *APE_LZ4_gpu_last_error(void);   /* thread-local message */
+const char *APE_LZ4_gpu_arch(void);         /* "gfx950" */
+
+/* ---- batched, device-resident, pointer-array form ----
+ * d_src[i]  : block i input (device)     d_srcSize[i] : its size (0..65536)
+ * d_dst[i]  : block i output (device)    d_dstCap[i]  : its capacity
+ * d_result[i] <- compressed size, or 0 if it does not fit d_dstCap[i]. */
+int APE_LZ4_compress_batch_dev(const char *const *d_src, const int *d_srcSize,
+                               char *const *d_dst, const int *d_dstCap, int *d_result,
+                               int nblocks, void *stream);
+
+/* d_result[i] <- decoded size, or -(consumed)-1, as APE_LZ4_decompress_safe. */
+int APE_LZ4_decompress_safe_batch_dev(const char *const *d_src, const int *d_compressedSize,
+                                      char *const *d_dst, const int *d_maxDecompressedSize,
+                                      int *d_result, int nblocks, void *stream);
+
+/* As APE_LZ4_decompress_safe_partial with per-block targetOutputSize. */
+int APE_LZ4_decompress_safe_partial_batch_dev(const char *const *d_src,
+                                              const int *d_compressedSize,
+                                              char *const *d_dst, const int *d_targetOutputSize,
+                                              const int *d_maxDecompressedSize,
+                                              int *d_result, int nblocks, void *stream);
+
+/* ---- batched, device-resident, strided form (block i at base + i*stride) ----
+ * The layout the benchmark uses: uncompressed slots of `src_stride` bytes,
+ * compressed slots of `dst_stride` bytes; a NULL cap array means
+ * "capacity = compressBound(srcSize)" / "= dst_stride". */
+int APE_LZ4_compress_batch_strided_dev(const char *d_src, size_t src_stride,
+                                       const int *d_srcSize, char *d_dst, size_t dst_stride,
+                                       const int *d_dstCap, int *d_result, int nblocks,
+                                       void *stream);
+int APE_LZ4_decompress_safe_batch_strided_dev(const char *d_src, size_t src_stride,
+                                              const int *d_compressedSize, char *d_dst,
+                                              size_t dst_stride,
+                                              const int *d_maxDecompressedSize,
+                                              int *d_result, int nblocks, void *stream);
+
+/* ---- host-buffer batch (socket / ape_buffer path): pinned staging, H2D,
+ * kernel, D2H on an internal stream; synchronous.  h_result as above. */
+int APE_LZ4_compress_batch_host(const char *const *h_src, const int *h_srcSize,
+                                char *const *h_dst, const int *h_dstCap, int *h_result,
+                                int nblocks);
+int APE_LZ4_decompress_safe_batch_host(const char *const *h_src, const int *h_compressedSize,
+                                       char *const *h_dst, const int *h_maxDecompressedSize,
+                                       int *h_result, int nblocks);
+
+/* ---- synthetic benchmark data, device-side ----
+ * kind 0 = random bytes, 1 = compressible; block b is seeded with first_block+b. */
+int APE_LZ4_synth_blocks_dev(char *d_out, size_t stride, int blockSize,
+                             long long first_block, int nblocks, int kind, void *stream);
+
+#if defined(__cplusplus)
+}
+#endif

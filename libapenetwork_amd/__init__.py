@@ -1,0 +1,176 @@
+"""libapenetwork_amd -- MI355X-native LZ4 block codec behind libapenetwork's ape_lz4.h.
+
+The product is the C shared library ``libape_lz4_amd.so`` built next to this file
+(``make -C libapenetwork_amd/csrc``): it exports the reference's ape_lz4.h ABI
+(src/ape_lz4.h:59-467) with the one-shot block codec running as HIP kernels, and
+the batched device API of include/ape_lz4_gpu.h.  This module is a thin ctypes
+mirror of that ABI for tests and the benchmark -- same function names, same
+argument meaning, same return conventions.  There is no Python or CPU fallback:
+importing works anywhere, but every call that needs the library raises if it is
+missing, and GPU entry points return the library's error codes without a GPU.
+"""
+import ctypes as _C
+import os as _os
+
+__all__ = [
+    "lib", "versionNumber", "compressBound", "compress_default", "compress_fast",
+    "decompress_safe", "decompress_safe_partial", "compress_batch", "decompress_batch",
+    "decompress_partial_batch", "synth_blocks", "gpu_init", "gpu_last_error", "GpuError",
+    "MAX_BLOCK", "ERANGE",
+]
+
+_HERE = _os.path.dirname(_os.path.abspath(__file__))
+LIB_PATH = _os.path.join(_HERE, "libape_lz4_amd.so")
+MAX_BLOCK = 65536
+ERANGE = -2147483648
+
+_lib = None
+
+
+class GpuError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libape_lz4_amd.so (raises OSError with the build command if absent)."""
+    global _lib
+    if _lib is None:
+        if not _os.path.exists(LIB_PATH):
+            raise OSError("libape_lz4_amd.so not built: run `make -C %s/csrc` "
+                          "(or __graft_entry__.build())" % _HERE)
+        L = _C.CDLL(LIB_PATH)
+        i, p, cp = _C.c_int, _C.c_void_p, _C.c_char_p
+        sz, ll = _C.c_size_t, _C.c_longlong
+        sig = {
+            "APE_LZ4_versionNumber": (i, []),
+            "APE_LZ4_compressBound": (i, [i]),
+            "APE_LZ4_compress_default": (i, [p, p, i, i]),
+            "APE_LZ4_compress_fast": (i, [p, p, i, i, i]),
+            "APE_LZ4_decompress_safe": (i, [p, p, i, i]),
+            "APE_LZ4_decompress_safe_partial": (i, [p, p, i, i, i]),
+            "APE_LZ4_gpu_init": (i, []),
+            "APE_LZ4_gpu_device_count": (i, []),
+            "APE_LZ4_gpu_last_error": (cp, []),
+            "APE_LZ4_compress_batch_dev": (i, [p, p, p, p, p, i, p]),
+            "APE_LZ4_decompress_safe_batch_dev": (i, [p, p, p, p, p, i, p]),
+            "APE_LZ4_decompress_safe_partial_batch_dev": (i, [p, p, p, p, p, p, i, p]),
+            "APE_LZ4_compress_batch_strided_dev": (i, [p, sz, p, p, sz, p, p, i, p]),
+            "APE_LZ4_decompress_safe_batch_strided_dev": (i, [p, sz, p, p, sz, p, p, i, p]),
+            "APE_LZ4_synth_blocks_dev": (i, [p, sz, i, ll, i, i, p]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+def versionNumber():
+    return lib().APE_LZ4_versionNumber()
+
+
+def compressBound(n):
+    return lib().APE_LZ4_compressBound(n)
+
+
+def gpu_init():
+    return lib().APE_LZ4_gpu_init()
+
+
+def gpu_last_error():
+    s = lib().APE_LZ4_gpu_last_error()
+    return s.decode() if s else ""
+
+
+def _buf(b, pad=16):
+    return _C.create_string_buffer(bytes(b) + b"\0" * pad, len(b) + pad)
+
+
+# ---- one-shot ape_lz4.h calls (host buffers; GPU inside) ----
+def compress_default(src, max_dst=None):
+    """APE_LZ4_compress_default: returns (ret, compressed_bytes)."""
+    cap = compressBound(len(src)) if max_dst is None else max_dst
+    out = _C.create_string_buffer(max(cap, 1))
+    r = lib().APE_LZ4_compress_default(_buf(src), out, len(src), cap)
+    return r, out.raw[:max(r, 0)]
+
+
+def compress_fast(src, max_dst=None, acceleration=1):
+    cap = compressBound(len(src)) if max_dst is None else max_dst
+    out = _C.create_string_buffer(max(cap, 1))
+    r = lib().APE_LZ4_compress_fast(_buf(src), out, len(src), cap, acceleration)
+    return r, out.raw[:max(r, 0)]
+
+
+def decompress_safe(comp, max_out):
+    """APE_LZ4_decompress_safe: returns (ret, dst[0:ret])."""
+    out = _C.create_string_buffer(max(max_out, 1))
+    r = lib().APE_LZ4_decompress_safe(_buf(comp), out, len(comp), max_out)
+    return r, out.raw[:max(r, 0)]
+
+
+def decompress_safe_partial(comp, target, max_out):
+    out = _C.create_string_buffer(max(max_out, 1))
+    r = lib().APE_LZ4_decompress_safe_partial(_buf(comp), out, len(comp), target, max_out)
+    return r, out.raw[:max(r, 0)]
+
+
+# ---- batched device API on torch tensors (device-resident) ----
+def _ptr(t):
+    return None if t is None else _C.c_void_p(t.data_ptr())
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return _C.c_void_p(stream.cuda_stream)
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise GpuError("%s failed (%d): %s" % (what, rc, gpu_last_error()))
+
+
+def compress_batch(src, src_sizes, dst, results, dst_caps=None, stream=None):
+    """N x APE_LZ4_compress_default on device.
+
+    src: uint8 [N, S] CUDA tensor (block i = row i, first src_sizes[i] bytes);
+    dst: uint8 [N, D] CUDA tensor; results: int32 [N] (compressed size or 0).
+    """
+    n = src.shape[0]
+    _check(lib().APE_LZ4_compress_batch_strided_dev(
+        _ptr(src), src.stride(0), _ptr(src_sizes), _ptr(dst), dst.stride(0), _ptr(dst_caps),
+        _ptr(results), n, _stream(stream)), "APE_LZ4_compress_batch_strided_dev")
+
+
+def decompress_batch(comp, comp_sizes, dst, results, dst_caps=None, stream=None):
+    """N x APE_LZ4_decompress_safe on device (caps default to dst row stride)."""
+    n = comp.shape[0]
+    _check(lib().APE_LZ4_decompress_safe_batch_strided_dev(
+        _ptr(comp), comp.stride(0), _ptr(comp_sizes), _ptr(dst), dst.stride(0), _ptr(dst_caps),
+        _ptr(results), n, _stream(stream)), "APE_LZ4_decompress_safe_batch_strided_dev")
+
+
+def decompress_partial_batch(src_ptrs, comp_sizes, dst_ptrs, targets, caps, results,
+                             stream=None):
+    """N x APE_LZ4_decompress_safe_partial, pointer-array form (int64 tensors of pointers)."""
+    n = comp_sizes.shape[0]
+    _check(lib().APE_LZ4_decompress_safe_partial_batch_dev(
+        _ptr(src_ptrs), _ptr(comp_sizes), _ptr(dst_ptrs), _ptr(targets), _ptr(caps),
+        _ptr(results), n, _stream(stream)), "APE_LZ4_decompress_safe_partial_batch_dev")
+
+
+def decompress_ptr_batch(src_ptrs, comp_sizes, dst_ptrs, caps, results, stream=None):
+    """N x APE_LZ4_decompress_safe, pointer-array form."""
+    n = comp_sizes.shape[0]
+    _check(lib().APE_LZ4_decompress_safe_batch_dev(
+        _ptr(src_ptrs), _ptr(comp_sizes), _ptr(dst_ptrs), _ptr(caps), _ptr(results), n,
+        _stream(stream)), "APE_LZ4_decompress_safe_batch_dev")
+
+
+def synth_blocks(dst, block_size, first_block, kind, stream=None):
+    """Fill rows of uint8 [N, S] CUDA tensor with SURVEY App. C blocks (kind 0 rand, 1 comp)."""
+    _check(lib().APE_LZ4_synth_blocks_dev(_ptr(dst), dst.stride(0), block_size, first_block,
+                                          dst.shape[0], kind, _stream(stream)),
+           "APE_LZ4_synth_blocks_dev")

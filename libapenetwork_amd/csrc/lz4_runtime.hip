@@ -1,0 +1,346 @@
+// lz4_runtime.hip -- the thin C-ABI shim between the C host code and the HIP
+// kernels: device checks, the batched launchers of include/ape_lz4_gpu.h, and
+// the pinned-staging host path used by the one-shot ape_lz4.h calls.
+//
+// No CPU fallback anywhere: without a usable gfx950 device every entry point
+// returns APE_LZ4_GPU_ENODEV (and the one-shot API reports failure).
+#include <mutex>
+#include <stdio.h>
+#include <string.h>
+#include <vector>
+
+#include "../../include/ape_lz4_gpu.h"
+#include "lz4_gpu_internal.h"
+#include "lz4_gpu_shim.h"
+
+using namespace apelz4;
+
+namespace {
+
+thread_local char g_err[256] = "";
+
+void set_err(const char *what, hipError_t e) {
+    snprintf(g_err, sizeof g_err, "%s: %s", what, e == hipSuccess ? "ok" : hipGetErrorString(e));
+}
+
+int g_ndev = -1;
+std::vector<int> g_dev_ok;  // per device: 1 = gfx950
+std::once_flag g_once;
+
+void probe() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    g_ndev = n;
+    g_dev_ok.assign(n > 0 ? n : 0, 0);
+    for (int d = 0; d < n; d++) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, d) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0)
+            g_dev_ok[d] = 1;
+    }
+}
+
+int check_device() {
+    std::call_once(g_once, probe);
+    if (g_ndev <= 0) {
+        snprintf(g_err, sizeof g_err, "no HIP device visible (libape_lz4_amd needs an MI355X)");
+        return APE_LZ4_GPU_ENODEV;
+    }
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= g_ndev || !g_dev_ok[d]) {
+        snprintf(g_err, sizeof g_err, "current HIP device %d is not gfx950 (MI355X)", d);
+        return APE_LZ4_GPU_ENODEV;
+    }
+    return APE_LZ4_GPU_OK;
+}
+
+int finish_launch(hipError_t e, const char *what) {
+    if (e != hipSuccess) {
+        set_err(what, e);
+        return APE_LZ4_GPU_ELAUNCH;
+    }
+    return APE_LZ4_GPU_OK;
+}
+
+// ---- per-thread pinned staging for the host-buffer path ----
+struct HostCtx {
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    char *h = nullptr;  // pinned
+    size_t hcap = 0;
+    char *d = nullptr;  // device
+    size_t dcap = 0;
+    // Trivially destructible on purpose: HIP may already be torn down when
+    // thread-exit destructors run; the staging is released on device change.
+    void release() {
+        if (h) (void)hipHostFree(h);
+        if (d) (void)hipFree(d);
+        if (stream) (void)hipStreamDestroy(stream);
+        *this = HostCtx();
+    }
+};
+thread_local HostCtx g_host;
+
+int host_reserve(size_t bytes) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (g_host.dev != dev) {
+        g_host.release();
+        g_host.dev = dev;
+        hipError_t e = hipStreamCreateWithFlags(&g_host.stream, hipStreamNonBlocking);
+        if (e != hipSuccess) { set_err("hipStreamCreate", e); return APE_LZ4_GPU_ENOMEM; }
+    }
+    if (g_host.hcap < bytes) {
+        if (g_host.h) (void)hipHostFree(g_host.h);
+        g_host.h = nullptr;
+        size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
+        hipError_t e = hipHostMalloc((void **)&g_host.h, cap, hipHostMallocDefault);
+        if (e != hipSuccess) { g_host.hcap = 0; set_err("hipHostMalloc", e); return APE_LZ4_GPU_ENOMEM; }
+        g_host.hcap = cap;
+    }
+    if (g_host.dcap < bytes) {
+        if (g_host.d) (void)hipFree(g_host.d);
+        g_host.d = nullptr;
+        size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
+        hipError_t e = hipMalloc((void **)&g_host.d, cap);
+        if (e != hipSuccess) { g_host.dcap = 0; set_err("hipMalloc", e); return APE_LZ4_GPU_ENOMEM; }
+        g_host.dcap = cap;
+    }
+    return APE_LZ4_GPU_OK;
+}
+
+inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// Staging layout (same offsets on host and device):
+//   [ptr arrays: src, dst][int arrays: in_size, cap, target, result][inputs][outputs]
+// mode: 0 = compress, 1 = decompress_safe, 2 = decompress_safe_partial
+int host_batch(int mode, const char *const *h_src, const int *h_in, char *const *h_dst,
+               const int *h_cap, const int *h_target, int *h_res, int nb) {
+    if (nb < 0 || (nb > 0 && (!h_src || !h_in || !h_dst || !h_cap || !h_res))) {
+        snprintf(g_err, sizeof g_err, "invalid argument");
+        return APE_LZ4_GPU_EINVAL;
+    }
+    int rc = check_device();
+    if (rc) return rc;
+    if (nb == 0) return APE_LZ4_GPU_OK;
+    std::vector<size_t> in_off(nb), out_off(nb), out_len(nb);
+    size_t meta = up16((size_t)nb * 2 * sizeof(void *)) + up16((size_t)nb * 4 * sizeof(int));
+    size_t pos = meta;
+    for (int i = 0; i < nb; i++) {
+        in_off[i] = pos;
+        size_t len = h_in[i] > 0 ? (size_t)h_in[i] : 1;  // size <= 0 still reads src[0]
+        pos += up16(len);
+    }
+    for (int i = 0; i < nb; i++) {
+        out_off[i] = pos;
+        size_t lim;
+        if (mode == 0) {
+            int n = h_in[i] > 0 ? h_in[i] : 0;
+            size_t bound = (size_t)n + n / 255 + 16;
+            lim = h_cap[i] <= 0 ? 0 : ((size_t)h_cap[i] < bound ? (size_t)h_cap[i] : bound);
+        } else {
+            lim = h_cap[i] <= 0 ? 0 : ((size_t)h_cap[i] < (size_t)kMaxBlock ? (size_t)h_cap[i]
+                                                                         : (size_t)kMaxBlock);
+        }
+        out_len[i] = lim;
+        pos += up16(lim ? lim : 1);
+    }
+    const size_t total = pos;
+    rc = host_reserve(total);
+    if (rc) return rc;
+    char *H = g_host.h, *D = g_host.d;
+    const char **hp_src = (const char **)H;
+    char **hp_dst = (char **)(H + (size_t)nb * sizeof(void *));
+    int *hi = (int *)(H + up16((size_t)nb * 2 * sizeof(void *)));
+    int *h_size = hi, *h_capd = hi + nb, *h_tgt = hi + 2 * nb;
+    const size_t ioff = up16((size_t)nb * 2 * sizeof(void *));
+    for (int i = 0; i < nb; i++) {
+        hp_src[i] = D + in_off[i];
+        hp_dst[i] = D + out_off[i];
+        h_size[i] = h_in[i];
+        h_capd[i] = h_cap[i];
+        h_tgt[i] = h_target ? h_target[i] : 0;
+        if (h_in[i] > 0) memcpy(H + in_off[i], h_src[i], (size_t)h_in[i]);
+        else H[in_off[i]] = h_src[i] ? h_src[i][0] : 0;
+    }
+    hipStream_t s = g_host.stream;
+    hipError_t e = hipMemcpyAsync(D, H, out_off[0], hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return finish_launch(e, "hipMemcpyAsync H2D");
+    BlockArgs a{};
+    a.src = (const char *const *)D;
+    a.dst = (char *const *)(D + (size_t)nb * sizeof(void *));
+    a.src_size = (const int *)(D + ioff);
+    a.dst_cap = (const int *)(D + ioff) + nb;
+    a.target = (const int *)(D + ioff) + 2 * nb;
+    a.result = (int *)(D + ioff) + 3 * nb;
+    a.nblocks = nb;
+    e = (mode == 0) ? launch_encode(a, s) : launch_decode(a, mode == 2, s);
+    if (e != hipSuccess) return finish_launch(e, "kernel launch");
+    e = hipMemcpyAsync(H + ioff + 3 * nb * sizeof(int), (const char *)a.result, nb * sizeof(int),
+                       hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(H + out_off[0], D + out_off[0], total - out_off[0],
+                           hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return finish_launch(e, "D2H / synchronize");
+    const int *hres = (const int *)(H + ioff) + 3 * nb;
+    for (int i = 0; i < nb; i++) {
+        h_res[i] = hres[i];
+        if (hres[i] > 0 && (size_t)hres[i] <= out_len[i]) memcpy(h_dst[i], H + out_off[i], hres[i]);
+    }
+    return APE_LZ4_GPU_OK;
+}
+
+BlockArgs ptr_args(const char *const *src, const int *in, char *const *dst, const int *cap,
+                   const int *tgt, int *res, int nb) {
+    BlockArgs a{};
+    a.src = src;
+    a.dst = dst;
+    a.src_size = in;
+    a.dst_cap = cap;
+    a.target = tgt;
+    a.result = res;
+    a.nblocks = nb;
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+int APE_LZ4_gpu_init(void) { return check_device(); }
+
+int APE_LZ4_gpu_device_count(void) {
+    std::call_once(g_once, probe);
+    return g_ndev < 0 ? 0 : g_ndev;
+}
+
+const char *APE_LZ4_gpu_last_error(void) { return g_err; }
+const char *APE_LZ4_gpu_arch(void) { return "gfx950"; }
+
+int APE_LZ4_compress_batch_dev(const char *const *d_src, const int *d_srcSize,
+                               char *const *d_dst, const int *d_dstCap, int *d_result,
+                               int nblocks, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_srcSize || !d_dst || !d_dstCap || !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    return finish_launch(launch_encode(ptr_args(d_src, d_srcSize, d_dst, d_dstCap, nullptr,
+                                                d_result, nblocks),
+                                       (hipStream_t)stream),
+                         "lz4_encode_kernel");
+}
+
+int APE_LZ4_decompress_safe_batch_dev(const char *const *d_src, const int *d_compressedSize,
+                                      char *const *d_dst, const int *d_maxDecompressedSize,
+                                      int *d_result, int nblocks, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_compressedSize || !d_dst ||
+                                         !d_maxDecompressedSize || !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    return finish_launch(launch_decode(ptr_args(d_src, d_compressedSize, d_dst,
+                                                d_maxDecompressedSize, nullptr, d_result, nblocks),
+                                       false, (hipStream_t)stream),
+                         "lz4_decode_kernel");
+}
+
+int APE_LZ4_decompress_safe_partial_batch_dev(const char *const *d_src,
+                                              const int *d_compressedSize, char *const *d_dst,
+                                              const int *d_targetOutputSize,
+                                              const int *d_maxDecompressedSize, int *d_result,
+                                              int nblocks, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_compressedSize || !d_dst ||
+                                         !d_targetOutputSize || !d_maxDecompressedSize ||
+                                         !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    return finish_launch(launch_decode(ptr_args(d_src, d_compressedSize, d_dst,
+                                                d_maxDecompressedSize, d_targetOutputSize,
+                                                d_result, nblocks),
+                                       true, (hipStream_t)stream),
+                         "lz4_decode_kernel<partial>");
+}
+
+int APE_LZ4_compress_batch_strided_dev(const char *d_src, size_t src_stride, const int *d_srcSize,
+                                       char *d_dst, size_t dst_stride, const int *d_dstCap,
+                                       int *d_result, int nblocks, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_srcSize || !d_dst || !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    if (!d_dstCap && dst_stride > 0x7FFFFFFF) return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    BlockArgs a{};
+    a.src_base = d_src;
+    a.dst_base = d_dst;
+    a.src_stride = src_stride;
+    a.dst_stride = dst_stride;
+    a.src_size = d_srcSize;
+    a.dst_cap = d_dstCap;
+    a.result = d_result;
+    a.nblocks = nblocks;
+    return finish_launch(launch_encode(a, (hipStream_t)stream), "lz4_encode_kernel");
+}
+
+int APE_LZ4_decompress_safe_batch_strided_dev(const char *d_src, size_t src_stride,
+                                              const int *d_compressedSize, char *d_dst,
+                                              size_t dst_stride, const int *d_maxDecompressedSize,
+                                              int *d_result, int nblocks, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_compressedSize || !d_dst || !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    if (!d_maxDecompressedSize && dst_stride > 0x7FFFFFFF) return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    BlockArgs a{};
+    a.src_base = d_src;
+    a.dst_base = d_dst;
+    a.src_stride = src_stride;
+    a.dst_stride = dst_stride;
+    a.src_size = d_compressedSize;
+    a.dst_cap = d_maxDecompressedSize;
+    a.result = d_result;
+    a.nblocks = nblocks;
+    return finish_launch(launch_decode(a, false, (hipStream_t)stream), "lz4_decode_kernel");
+}
+
+int APE_LZ4_compress_batch_host(const char *const *h_src, const int *h_srcSize,
+                                char *const *h_dst, const int *h_dstCap, int *h_result,
+                                int nblocks) {
+    return host_batch(0, h_src, h_srcSize, h_dst, h_dstCap, nullptr, h_result, nblocks);
+}
+
+int APE_LZ4_decompress_safe_batch_host(const char *const *h_src, const int *h_compressedSize,
+                                       char *const *h_dst, const int *h_maxDecompressedSize,
+                                       int *h_result, int nblocks) {
+    return host_batch(1, h_src, h_compressedSize, h_dst, h_maxDecompressedSize, nullptr,
+                      h_result, nblocks);
+}
+
+int APE_LZ4_synth_blocks_dev(char *d_out, size_t stride, int blockSize, long long first_block,
+                             int nblocks, int kind, void *stream) {
+    if (nblocks < 0 || blockSize < 0 || blockSize > kMaxBlock || (nblocks > 0 && !d_out) ||
+        stride < (size_t)blockSize)
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    return finish_launch(launch_synth(d_out, stride, blockSize, first_block, nblocks, kind,
+                                      (hipStream_t)stream),
+                         "lz4_synth_kernel");
+}
+
+// ---- internal shim for the one-shot C API (ape_lz4_api.c) ----
+int ape_lz4_gpu_compress_one(const char *src, char *dst, int n, int cap, int *rt) {
+    int res = 0;
+    *rt = host_batch(0, &src, &n, &dst, &cap, nullptr, &res, 1);
+    return res;
+}
+
+int ape_lz4_gpu_decompress_one(const char *src, char *dst, int csize, int cap, int partial,
+                               int target, int *rt) {
+    int res = 0;
+    *rt = host_batch(partial ? 2 : 1, &src, &csize, &dst, &cap, partial ? &target : nullptr,
+                     &res, 1);
+    return res;
+}
+
+}  // extern "C"

@@ -1,0 +1,123 @@
+/*
+ * cpu_bench.c -- TEST INFRASTRUCTURE: the CPU baseline of bench.py.
+ *
+ * Times a codec's compress_default + decompress_safe over a bounded sample of
+ * independent blocks with a static block partition over `nthreads` pthreads
+ * (one block = one task, as BASELINE.md section 4 prescribes).  The codec is
+ * loaded with dlopen: either the reference itself (oracle/_ref/libape_lz4_ref.so,
+ * symbol prefix "APE_LZ4_", kind "reference") or the oracle restatement
+ * (oracle/liblz4_oracle.so, prefix "orc_", kind "port").
+ */
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+typedef int (*comp_fn)(const char *, char *, int, int);
+typedef int (*dec_fn)(const char *, char *, int, int);
+
+void synth_blocks(uint8_t *out, int n, long long stride, long long first_block, int nblocks,
+                  int kind);
+
+typedef struct {
+    comp_fn comp;
+    dec_fn dec;
+    const uint8_t *in;
+    uint8_t *cmp, *out;
+    int *csz;
+    int n, cap, b0, b1, phase, bad;
+} task_t;
+
+static void *worker(void *arg)
+{
+    task_t *t = (task_t *)arg;
+    for (int b = t->b0; b < t->b1; b++) {
+        const char *src = (const char *)t->in + (long long)b * t->n;
+        char *c = (char *)t->cmp + (long long)b * t->cap;
+        if (t->phase == 0) {
+            t->csz[b] = t->comp(src, c, t->n, t->cap);
+        } else {
+            char *o = (char *)t->out + (long long)b * t->n;
+            int r = t->dec(c, o, t->csz[b], t->n);
+            if (r != t->n) t->bad++;
+        }
+    }
+    return NULL;
+}
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+static double run_phase(task_t *tasks, int nthreads, int phase)
+{
+    pthread_t th[256];
+    double t0 = now_s();
+    for (int i = 0; i < nthreads; i++) {
+        tasks[i].phase = phase;
+        pthread_create(&th[i], NULL, worker, &tasks[i]);
+    }
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    return now_s() - t0;
+}
+
+/*
+ * Returns 0 on success.  out[0] = compress seconds, out[1] = decompress seconds,
+ * out[2] = total compressed bytes, out[3] = round-trip failures,
+ * out[4] = uncompressed bytes.  `reps` timed repetitions (after one warm-up),
+ * times are summed over reps.
+ */
+int cpu_bench_run(const char *lib, const char *prefix, int nthreads, int nblocks, int n,
+                  int kind, int reps, double *out)
+{
+    char name[128];
+    void *h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+    if (!h) { fprintf(stderr, "cpu_bench: %s\n", dlerror()); return -1; }
+    snprintf(name, sizeof name, "%scompress_default", prefix);
+    comp_fn comp = (comp_fn)dlsym(h, name);
+    snprintf(name, sizeof name, "%sdecompress_safe", prefix);
+    dec_fn dec = (dec_fn)dlsym(h, name);
+    if (!comp || !dec || nthreads < 1 || nthreads > 256) return -2;
+    int cap = n + n / 255 + 16;
+    uint8_t *in = malloc((size_t)nblocks * n);
+    uint8_t *cmp = malloc((size_t)nblocks * cap);
+    uint8_t *o = malloc((size_t)nblocks * n);
+    int *csz = calloc((size_t)nblocks, sizeof(int));
+    if (!in || !cmp || !o || !csz) return -3;
+    synth_blocks(in, n, n, 0, nblocks, kind);
+    memset(cmp, 0, (size_t)nblocks * cap); /* pre-fault */
+    memset(o, 0, (size_t)nblocks * n);
+    task_t tasks[256];
+    for (int i = 0; i < nthreads; i++) {
+        tasks[i] = (task_t){comp, dec, in, cmp, o, csz, n, cap,
+                            (int)((long long)nblocks * i / nthreads),
+                            (int)((long long)nblocks * (i + 1) / nthreads), 0, 0};
+    }
+    run_phase(tasks, nthreads, 0); /* warm-up */
+    run_phase(tasks, nthreads, 1);
+    double tc = 0, td = 0;
+    for (int r = 0; r < reps; r++) {
+        tc += run_phase(tasks, nthreads, 0);
+        td += run_phase(tasks, nthreads, 1);
+    }
+    long long tot = 0;
+    int bad = 0;
+    for (int b = 0; b < nblocks; b++) tot += csz[b];
+    for (int i = 0; i < nthreads; i++) bad += tasks[i].bad;
+    if (memcmp(in, o, (size_t)nblocks * n) != 0) bad++;
+    out[0] = tc;
+    out[1] = td;
+    out[2] = (double)tot;
+    out[3] = bad;
+    out[4] = (double)nblocks * n;
+    free(in); free(cmp); free(o); free(csz);
+    dlclose(h);
+    return 0;
+}

@@ -1,0 +1,141 @@
+"""GPU decoder parity: bit-exact with the reference decompress_safe / _partial.
+
+The bar (tier contract): identical return value for every block -- including the
+negative -(consumed)-1 codes of malformed streams -- and identical dst[0:ret].
+Streams with a zero match offset are excluded from content comparison only (the
+reference then copies uninitialised dst bytes).
+"""
+import base64
+import random
+
+import pytest
+
+from gpuutil import alloc_out, fetch, ints, pack
+from lz4util import I, orc_compress, orc_decompress, sha
+
+pytestmark = pytest.mark.gpu
+
+
+def run_decode(torch, amd, comps, caps, targets=None, in_mis=None, out_mis=None):
+    src, sptr, _ = pack(torch, comps, misalign=in_mis)
+    dst, dptr, doffs = alloc_out(torch, caps, misalign=out_mis)
+    res = ints(torch, [0] * len(comps))
+    if targets is None:
+        amd.decompress_ptr_batch(sptr, ints(torch, map(len, comps)), dptr, ints(torch, caps), res)
+    else:
+        amd.decompress_partial_batch(sptr, ints(torch, map(len, comps)), dptr,
+                                     ints(torch, targets), ints(torch, caps), res)
+    torch.cuda.synchronize()
+    rs = res.cpu().tolist()
+    outs = [fetch(dst, o, r) for o, r in zip(doffs, rs)]
+    return rs, outs
+
+
+def test_golden_decode_kats(cuda, product, golden):
+    cases = golden["decode"]
+    comps = [base64.b64decode(d["comp_b64"]) for d in cases]
+    caps = [d["cap"] for d in cases]
+    rs, outs = run_decode(cuda, product, comps, caps)
+    for d, r, out in zip(cases, rs, outs):
+        assert r == d["ret"], d["name"]
+        if r > 0 and not d["has_offset0"]:
+            assert sha(out) == d["out_sha256"], d["name"]
+    tg = [d["partial"]["target"] for d in cases]
+    rs, outs = run_decode(cuda, product, comps, caps, targets=tg)
+    for d, r, out in zip(cases, rs, outs):
+        assert r == d["partial"]["ret"], d["name"]
+        if r > 0 and not d["has_offset0"]:
+            assert sha(out) == d["partial"]["out_sha256"], d["name"]
+
+
+def test_roundtrip_reference_streams(cuda, product, oracle):
+    """Blocks compressed by the reference encoder decode bit-exactly on the GPU."""
+    srcs = []
+    for content in ("comp", "rand", "text", "zeros", "period3", "period7"):
+        for n in (65536, 4096, 8192, 1000, 13, 65535, 30000):
+            srcs.append(I.make(content, n, seed=n))
+    for b in range(24):
+        srcs.append(I.synth_comp(65536, 1000 + b))
+    comps = [orc_compress(oracle, s)[1] for s in srcs]
+    for caps in ([len(s) for s in srcs], [max(len(s) - 1, 0) for s in srcs],
+                 [len(s) + 17 for s in srcs]):
+        rs, outs = run_decode(cuda, product, comps, caps)
+        for s, c, cap, r, out in zip(srcs, comps, caps, rs, outs):
+            er, eout = orc_decompress(oracle, c, cap)
+            assert r == er, (len(s), cap)
+            if r > 0:
+                assert out == eout
+
+
+def test_fuzz_malformed_vs_oracle(cuda, product, oracle):
+    rng = random.Random(1234)
+    comps, caps, tg = [], [], []
+    for k in range(3000):
+        content = rng.choice(["comp", "text", "rand", "period3", "zeros", "byte"])
+        n = rng.choice([16, 64, 300, 1000, 4096, 8192, 20000, 65536])
+        _, c = orc_compress(oracle, I.make(content, n, seed=k))
+        c = bytearray(c)
+        for _ in range(rng.randrange(0, 5)):
+            if c:
+                c[rng.randrange(len(c))] = rng.randrange(256)
+        if rng.random() < 0.2:
+            c = c[:rng.randrange(len(c) + 1)]
+        comps.append(bytes(c))
+        caps.append(max(0, rng.choice([n, n - 1, n + 40, rng.randrange(n + 1), 65536])))
+        tg.append(rng.randrange(-5, n + 40))
+    for targets in (None, tg):
+        rs, outs = run_decode(cuda, product, comps, caps, targets=targets)
+        bad = []
+        for i, (c, cap, r, out) in enumerate(zip(comps, caps, rs, outs)):
+            er, eout = orc_decompress(oracle, c, cap, None if targets is None else targets[i])
+            if r != er or (r > 0 and out != eout and not _has_off0(c)):
+                bad.append((i, len(c), cap, r, er))
+        assert not bad, bad[:10]
+
+
+def _has_off0(c):
+    import gen_golden
+    return gen_golden.has_offset0(c)
+
+
+def test_misaligned_buffers(cuda, product, oracle):
+    rng = random.Random(5)
+    srcs = [I.make(rng.choice(["comp", "text", "rand"]), rng.randrange(1, 65537), seed=i)
+            for i in range(64)]
+    comps = [orc_compress(oracle, s)[1] for s in srcs]
+    rs, outs = run_decode(cuda, product, comps, [len(s) for s in srcs],
+                          in_mis=[i % 16 for i in range(64)], out_mis=[(i * 7) % 16 for i in range(64)])
+    assert rs == [len(s) for s in srcs]
+    assert outs == srcs
+
+
+def test_gpu_block_limit(cuda, product, oracle):
+    big = I.make("text", 70000)
+    _, c = orc_compress(oracle, big)
+    small = I.make("comp", 40000)
+    _, c2 = orc_compress(oracle, small)
+    rs, outs = run_decode(cuda, product, [c, c2], [70000, 70000])
+    assert rs[0] == product.ERANGE
+    assert rs[1] == 40000 and outs[1] == small
+
+
+def test_strided_batch_benchmark_layout(cuda, product, oracle):
+    """The layout bench.py uses: fixed-stride slots, caps from the stride."""
+    torch = cuda
+    nb, n = 64, 65536
+    slot = (n + n // 255 + 16 + 15) // 16 * 16
+    srcs = [I.synth_comp(n, b) for b in range(nb)]
+    comp = torch.zeros((nb, slot), dtype=torch.uint8, device="cuda")
+    csz = []
+    for b, s in enumerate(srcs):
+        r, c = orc_compress(oracle, s)
+        comp[b, :r] = torch.frombuffer(bytearray(c), dtype=torch.uint8).cuda()
+        csz.append(r)
+    out = torch.zeros((nb, n), dtype=torch.uint8, device="cuda")
+    res = ints(torch, [0] * nb)
+    product.decompress_batch(comp, ints(torch, csz), out, res)
+    torch.cuda.synchronize()
+    assert res.cpu().tolist() == [n] * nb
+    host = out.cpu().numpy()
+    for b in range(nb):
+        assert host[b].tobytes() == srcs[b]

@@ -1,0 +1,109 @@
+"""GPU encoder: emits valid LZ4 v1.7.1 blocks.
+
+Bar (north_star): the reference decompress_safe (the oracle restatement, pinned to
+the reference by tests/test_oracle_golden.py) restores the input exactly with
+cap = srcSize, the output never exceeds compressBound, limited-output semantics
+hold (0 when it does not fit), output is deterministic, and the compression
+ratio on the benchmark data is reported next to the reference's.
+"""
+import random
+
+import pytest
+
+from gpuutil import alloc_out, fetch, ints, pack
+from lz4util import I, orc_compress, orc_decompress, walk_ok
+
+pytestmark = pytest.mark.gpu
+
+
+def run_encode(torch, amd, srcs, caps=None, in_mis=None, out_mis=None):
+    caps = [amd.compressBound(len(s)) for s in srcs] if caps is None else caps
+    src, sptr, _ = pack(torch, srcs, misalign=in_mis)
+    dst, dptr, doffs = alloc_out(torch, caps, misalign=out_mis)
+    res = ints(torch, [0] * len(srcs))
+    rc = amd.lib().APE_LZ4_compress_batch_dev(
+        sptr.data_ptr(), ints(torch, map(len, srcs)).data_ptr(), dptr.data_ptr(),
+        ints(torch, caps).data_ptr(), res.data_ptr(), len(srcs), None)
+    assert rc == 0, amd.gpu_last_error()
+    torch.cuda.synchronize()
+    rs = res.cpu().tolist()
+    return rs, [fetch(dst, o, r) for o, r in zip(doffs, rs)]
+
+
+def check_valid(oracle, src, comp):
+    r, out = orc_decompress(oracle, comp, len(src))
+    assert r == len(src), (len(src), r)
+    assert out == src
+    walk_ok(comp)  # parses as a well-formed sequence list
+
+
+def test_golden_inputs_roundtrip(cuda, product, oracle):
+    srcs = []
+    for content in I.ENC_CONTENTS:
+        for n in I.ENC_SIZES:
+            if n <= 65536:
+                srcs.append(I.make(content, n))
+    rs, comps = run_encode(cuda, product, srcs)
+    for s, r, c in zip(srcs, rs, comps):
+        assert 0 < r <= product.compressBound(len(s)), len(s)
+        check_valid(oracle, s, c)
+
+
+def test_benchmark_blocks_ratio_and_roundtrip(cuda, product, oracle):
+    srcs = [I.synth_comp(65536, b) for b in range(64)] + \
+           [I.synth_rand(4096, b) for b in range(64)] + \
+           [I.synth_comp(4096, b) for b in range(64)]
+    rs, comps = run_encode(cuda, product, srcs)
+    ref = [orc_compress(oracle, s)[0] for s in srcs]
+    for s, c in zip(srcs, comps):
+        check_valid(oracle, s, c)
+    gpu_ratio = 64 * 65536 / sum(rs[:64])
+    ref_ratio = 64 * 65536 / sum(ref[:64])
+    print("64 KiB compressible ratio: gpu %.4f reference %.4f" % (gpu_ratio, ref_ratio))
+    assert gpu_ratio >= 0.97 * ref_ratio
+    assert rs[64:128] == [4114] * 64  # incompressible: one literal run, as the reference
+    # and the GPU decoder restores them too
+    from test_gpu_decode import run_decode
+    drs, outs = run_decode(cuda, product, comps, [len(s) for s in srcs])
+    assert drs == [len(s) for s in srcs] and outs == srcs
+
+
+def test_limited_output(cuda, product, oracle):
+    srcs = [I.make(c, n, seed=n) for c in ("comp", "text", "rand") for n in (100, 5000, 65536)]
+    rs, comps = run_encode(cuda, product, srcs)
+    rs2, comps2 = run_encode(cuda, product, srcs, caps=rs)
+    assert rs2 == rs and comps2 == comps
+    rs3, _ = run_encode(cuda, product, srcs, caps=[r - 1 for r in rs])
+    assert rs3 == [0] * len(srcs)
+
+
+def test_deterministic(cuda, product):
+    srcs = [I.synth_comp(65536, b) for b in range(16)] + [I.text(65536, 3)]
+    a = run_encode(cuda, product, srcs)
+    b = run_encode(cuda, product, srcs)
+    assert a == b
+
+
+def test_misaligned_and_random_sizes(cuda, product, oracle):
+    rng = random.Random(9)
+    srcs = [I.make(rng.choice(["comp", "text", "rand", "zeros", "period7"]),
+                   rng.randrange(0, 65537), seed=i) for i in range(96)]
+    rs, comps = run_encode(cuda, product, srcs, in_mis=[i % 16 for i in range(96)],
+                           out_mis=[(3 * i) % 16 for i in range(96)])
+    for s, c in zip(srcs, comps):
+        check_valid(oracle, s, c)
+
+
+def test_pathological_runs(cuda, product, oracle):
+    """Long matches exercise the cooperative extension path."""
+    srcs = [bytes(65536), b"\xab" * 65536, (b"xyz" * 30000)[:65536],
+            bytes(1000) + I.synth_rand(2000, 1) + bytes(62536)]
+    rs, comps = run_encode(cuda, product, srcs)
+    for s, c in zip(srcs, comps):
+        check_valid(oracle, s, c)
+    assert rs[0] < 400 and rs[1] < 400
+
+
+def test_block_limit(cuda, product):
+    rs, _ = run_encode(cuda, product, [bytes(65537)])
+    assert rs == [product.ERANGE]

@@ -1,0 +1,191 @@
+"""CPU tests of the product library (no GPU compute here).
+
+* libape_lz4_amd.so loads and exports every function include/*.h declares;
+* ABI sizes/constants match the reference (ape_lz4.h:52-59, 123-127, 240-253, 317-322);
+* the host stream codec (the socket TX/RX path) is bit-exact
+  with the reference on the golden stream KATs and with the oracle on dictionary /
+  prefix / fast decoding;
+* without a GPU the one-shot GPU entry points fail loudly (no CPU fallback).
+"""
+import base64
+import ctypes as C
+import os
+import random
+import re
+import subprocess
+
+import pytest
+
+from lz4util import I, buf, orc_compress, sha
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = []
+    for h in ("ape_lz4.h", "ape_lz4_gpu.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"#define[^\n]*(\\\n[^\n]*)*", "", src)
+        for m in re.finditer(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", src):
+            name = m.group(1)
+            if name.startswith(("APE_LZ4_", "LZ4_compress_forceExtDict")):
+                names.append(name)
+    return sorted(set(names))
+
+
+def test_exports_everything_declared(product):
+    L = product.lib()
+    names = declared_functions()
+    assert len(names) >= 40 + 12
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", product.LIB_PATH], capture_output=True,
+                         text=True).stdout
+    exported = set(line.split()[-1] for line in out.splitlines() if " T " in line)
+    assert set(names) <= exported
+
+
+def test_reference_symbol_set(product):
+    """The 40 symbols the reference library exports are all present."""
+    ref40 = """versionNumber compress_default decompress_safe compressBound compress_fast
+    sizeofState compress_fast_extState compress_destSize decompress_fast decompress_safe_partial
+    resetStream createStream freeStream loadDict compress_fast_continue saveDict
+    createStreamDecode freeStreamDecode setStreamDecode decompress_safe_continue
+    decompress_fast_continue decompress_safe_usingDict decompress_fast_usingDict compress
+    compress_limitedOutput compress_withState compress_limitedOutput_withState compress_continue
+    compress_limitedOutput_continue create sizeofStreamState resetStreamState slideInputBuffer
+    decompress_safe_withPrefix64k decompress_fast_withPrefix64k compress_fast_force
+    decompress_safe_forceExtDict uncompress uncompress_unknownOutputSize""".split()
+    names = ["APE_LZ4_" + n for n in ref40] + ["LZ4_compress_forceExtDict"]
+    assert len(names) == 40
+    L = product.lib()
+    assert all(hasattr(L, n) for n in names)
+
+
+def test_constants(product, golden):
+    L = product.lib()
+    assert product.versionNumber() == golden["version"] == 10701
+    assert L.APE_LZ4_sizeofState() == L.APE_LZ4_sizeofStreamState() == 16416
+    for n in (0, 1, 255, 4096, 65536, 0x7E000000, 0x7E000001, -1):
+        assert product.compressBound(n) == (0 if (n & 0xFFFFFFFF) > 0x7E000000 else n + n // 255 + 16)
+
+
+def _product_stream_frames(L, st):
+    L.APE_LZ4_createStream.restype = C.c_void_p
+    msgs = [I.make(st["content"], st["msg_len"], seed=s) for s in st["seeds"]]
+    s = C.c_void_p(L.APE_LZ4_createStream())
+    dictbuf = C.create_string_buffer(65536)
+    frames, keep = [], []
+    for msg in msgs:
+        mb = buf(msg)
+        keep.append(mb)
+        pos = 0
+        while pos < len(msg):
+            ln = min(8192, len(msg) - pos)
+            ob = C.create_string_buffer(8240 + 64)
+            r = L.APE_LZ4_compress_fast_continue(s, C.byref(mb, pos), ob, ln, 8240, 1)
+            frames.append(ob.raw[:r])
+            pos += ln
+        L.APE_LZ4_saveDict(s, dictbuf, 65536)
+    L.APE_LZ4_freeStream(s)
+    return frames
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2])
+def test_host_stream_codec_golden(product, golden, idx):
+    """Socket-style TX (compress_fast_continue + saveDict) and RX (safe_continue + ring)."""
+    L = product.lib()
+    st = golden["stream"][idx]
+    frames = _product_stream_frames(L, st)
+    assert [base64.b64encode(f).decode() for f in frames] == st["frames_b64"]
+    L.APE_LZ4_createStreamDecode.restype = C.c_void_p
+    ds = C.c_void_p(L.APE_LZ4_createStreamDecode())
+    ring = C.create_string_buffer(65536)
+    rp, rets, plain = 0, [], b""
+    for fr in frames:
+        tmp = C.create_string_buffer(8192 + 64)
+        r = L.APE_LZ4_decompress_safe_continue(ds, buf(fr), tmp, len(fr), 8192)
+        rets.append(r)
+        if r <= 0:
+            break
+        plain += tmp.raw[:r]
+        if rp + r > 65536:
+            keepn = 65536 - r
+            C.memmove(ring, C.byref(ring, rp - keepn), keepn)
+            rp = keepn
+        C.memmove(C.byref(ring, rp), tmp, r)
+        rp += r
+        L.APE_LZ4_setStreamDecode(ds, ring, rp)
+    L.APE_LZ4_freeStreamDecode(ds)
+    assert rets == st["dec_rets"] and sha(plain) == st["plain_sha256"]
+
+
+def test_host_dict_and_fast_decoders_vs_oracle(product, oracle):
+    """usingDict (ext + prefix forms), forceExtDict, withPrefix64k, decompress_fast,
+    fast_continue and compress_destSize against the oracle, incl. mutated input."""
+    L = product.lib()
+    rng = random.Random(77)
+    for it in range(120):
+        n1 = rng.choice([100, 4096, 8192, 65536])
+        msg = I.make(rng.choice(["comp", "text", "rand"]), n1 + 8192, seed=it)
+        # chunk 2 compressed against chunk 1 as an external dictionary
+        st = C.c_void_p(oracle.orc_createStream())
+        b1, b2 = buf(msg[:n1]), buf(msg[n1:])
+        c1 = C.create_string_buffer(n1 + n1 // 255 + 80)
+        oracle.orc_compress_fast_continue(st, b1, c1, n1, n1 + n1 // 255 + 16, 1)
+        c2 = C.create_string_buffer(8300)
+        k = oracle.orc_compress_fast_continue(st, b2, c2, 8192, 8240, 1)
+        comp = bytearray(c2.raw[:k])
+        if it % 3 == 2:
+            comp[rng.randrange(len(comp))] = rng.randrange(256)
+        comp = bytes(comp)
+        for name, call in (
+            ("safe_usingDict_ext", lambda lib, p, o: getattr(lib, p + "decompress_safe_usingDict")(
+                buf(comp), o, len(comp), 8192, b1, n1)),
+            ("safe_forceExtDict", lambda lib, p, o: getattr(lib, p + "decompress_safe_forceExtDict")(
+                buf(comp), o, len(comp), 8192, b1, n1)),
+        ):
+            outs = []
+            for lib, p in ((L, "APE_LZ4_"), (oracle, "orc_")):
+                o = C.create_string_buffer(8192 + 64)
+                r = call(lib, p, o)
+                outs.append((r, o.raw[:max(r, 0)]))
+            assert outs[0] == outs[1], (name, it)
+        # prefix form: dictionary immediately precedes dst
+        outs = []
+        for lib, p in ((L, "APE_LZ4_"), (oracle, "orc_")):
+            pre = buf(msg[:n1] + b"\0" * 8300)
+            r = getattr(lib, p + "decompress_safe_usingDict")(buf(comp), C.byref(pre, n1),
+                                                              len(comp), 8192, pre, n1)
+            outs.append((r, pre.raw[n1:n1 + max(r, 0)]))
+        assert outs[0] == outs[1]
+    # one-shot fast decoders and destSize
+    for it in range(200):
+        src = I.make(rng.choice(["comp", "text", "rand", "zeros"]), rng.randrange(1, 70000), seed=it)
+        _, comp = orc_compress(oracle, src)
+        tgt = rng.randrange(1, len(comp) + 20)
+        outs = []
+        for lib, p in ((L, "APE_LZ4_"), (oracle, "orc_")):
+            pad = C.create_string_buffer(65536 + len(src) + 64)
+            r1 = getattr(lib, p + "decompress_fast")(buf(comp), C.byref(pad, 65536), len(src))
+            r2 = getattr(lib, p + "decompress_safe_withPrefix64k")(buf(comp), C.byref(pad, 65536),
+                                                                    len(comp), len(src))
+            sz = C.c_int(len(src))
+            d = C.create_string_buffer(tgt + 64)
+            r3 = getattr(lib, p + "compress_destSize")(buf(src), d, C.byref(sz), tgt)
+            outs.append((r1, r2, pad.raw[65536:65536 + len(src)], r3, sz.value, d.raw[:max(r3, 0)]))
+        assert outs[0] == outs[1], it
+
+
+def test_no_gpu_fails_loudly(product):
+    """Without a device the GPU entry points report failure; nothing falls back to CPU."""
+    L = product.lib()
+    if L.APE_LZ4_gpu_device_count() > 0:
+        pytest.skip("a GPU is visible here; covered by the -m gpu suite")
+    assert product.gpu_init() == -1
+    assert "no HIP device" in product.gpu_last_error()
+    r, _ = product.compress_default(b"hello hello hello hello hello")
+    assert r == 0
+    r, _ = product.decompress_safe(b"\x50hello", 5)
+    assert r < 0
