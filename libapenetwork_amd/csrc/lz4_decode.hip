@@ -344,10 +344,17 @@ lz4_decode_kernel(BlockArgs a) {
         __syncthreads();
         if (S.state == T_DONE) break;
         if (tid == 0) {
+            // the chain always advances (>= 3 bytes per sequence); anything else is
+            // an internal error, reported rather than looped on
+            if (S.carry <= cbase || S.carry >= (uint32_t)c.csize) {
+                S.state = T_ERR;
+                S.result = kErange;
+            }
             S.cbase = S.carry;
             S.out0 = S.out_next;
         }
         __syncthreads();
+        if (S.state == T_ERR) break;
     }
 
     // 5. result + flush dst[0:result) with 16-byte stores
