@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""bench.py -- LZ4 GiB/s device-resident (compress+decompress), 1M x 64 KiB blocks.
+
+BASELINE.json metric / config 3 ("1M x 64 KiB compressible blocks, compress+decompress,
+1 MI355X"); with --gpus N under torch.distributed.run every rank processes its own
+1M-block shard (distinct blocks: block ids rank*N .. ), no collective on the data
+path, and the reported value is the whole-job aggregate (weak scaling).
+
+One step = compress every block (one launch of lz4_encode_kernel over all blocks)
+then decompress every compressed block (one launch of lz4_decode_kernel); inputs are
+generated on the device before timing (SURVEY App. C `gen_comp`, seed = block id).
+value = uncompressed bytes of all ranks / max-over-ranks step time.  Correctness is
+checked after timing (every decoded block == its source, sampled GPU-compressed blocks
+restored by the oracle = the reference decoder restated), and the compression ratio
+is reported beside the throughput.
+
+roofline: the dominant kernel's algorithmic bytes (encode: n + c per block, decode:
+c + n) per launch / its average duration from HIP events on the launch stream.
+cpu_baseline: the reference src/ape_lz4.c (oracle/_ref, built from the reference
+sources) -- or the oracle restatement if absent -- timed on this host's cores over a
+bounded sample of the same workload, rank 0 at N=1 only.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table (8.0 TB/s spec)
+METRIC = "LZ4 GiB/s device-resident (compress+decompress), 1M×64KiB blocks, 1/2/4/8 GPU"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(block, kind, target_s):
+    """Reference codec on host cores, compress_default + decompress_safe per block."""
+    lib = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
+    lib.cpu_bench_run.restype = C.c_int
+    lib.cpu_bench_run.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.c_int, C.POINTER(C.c_double)]
+    ref = os.path.join(ROOT, "oracle", "_ref", "libape_lz4_ref.so")
+    if os.path.exists(ref):
+        path, prefix, kindname = ref, b"APE_LZ4_", "reference"
+    else:
+        path, prefix, kindname = os.path.join(ROOT, "oracle", "liblz4_oracle.so"), b"orc_", "port"
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    out = (C.c_double * 5)()
+    # calibrate on a small sample, then size the sample for ~target_s of wall time
+    nb = 1024
+    rc = lib.cpu_bench_run(path.encode(), prefix, threads, nb, block, kind, 1, out)
+    if rc != 0:
+        return None
+    per_block = (out[0] + out[1]) / nb
+    nb = int(min(32768, max(1024, target_s / max(per_block, 1e-9) / 2)))
+    reps = max(1, int(target_s / max(per_block * nb, 1e-9)))
+    rc = lib.cpu_bench_run(path.encode(), prefix, threads, nb, block, kind, reps, out)
+    if rc != 0 or out[3] != 0:
+        return None
+    tc, td, csz, bytes_ = out[0], out[1], out[2], out[4]
+    return {
+        "value": round(bytes_ * reps / (tc + td) / GIB, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": kindname,
+        "sample": "%d x %d KiB %s blocks x %d reps, compress_default + decompress_safe, "
+                  "%d threads (static block partition), %.1f s" % (
+                      nb, block >> 10, "compressible" if kind else "random", reps, threads,
+                      tc + td),
+        "compress_GiBps": round(bytes_ * reps / tc / GIB, 3),
+        "decompress_GiBps": round(bytes_ * reps / td / GIB, 3),
+        "ratio": round(bytes_ / csz, 4),
+    }
+
+
+def pmc_traffic(kernel, blocks):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass, scaled per block."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))[kernel]
+        return int(d["bytes_per_block"] * blocks)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--blocks", type=int, default=1 << 20, help="blocks per rank")
+    ap.add_argument("--block-size", type=int, default=65536)
+    ap.add_argument("--kind", choices=["comp", "rand"], default="comp")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify-sample", type=int, default=64)
+    args = ap.parse_args()
+
+    import torch
+
+    import libapenetwork_amd as amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rc = amd.gpu_init()
+    if rc != 0:
+        raise SystemExit("GPU codec unavailable: %s" % amd.gpu_last_error())
+
+    n, nb = args.block_size, args.blocks
+    kind = 1 if args.kind == "comp" else 0
+    slot = (amd.compressBound(n) + 15) // 16 * 16
+    stream = torch.cuda.current_stream()
+    log("[rank %d] allocating %.1f GiB (in %d x %d, slots %d)" % (
+        rank, nb * (2 * n + slot) / GIB, nb, n, slot))
+    src = torch.empty((nb, n), dtype=torch.uint8, device="cuda")
+    comp = torch.empty((nb, slot), dtype=torch.uint8, device="cuda")
+    out = torch.empty((nb, n), dtype=torch.uint8, device="cuda")
+    sizes = torch.full((nb,), n, dtype=torch.int32, device="cuda")
+    csz = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    dres = torch.zeros(nb, dtype=torch.int32, device="cuda")
+
+    t0 = time.time()
+    chunk = 1 << 16
+    first = rank * nb
+    for b0 in range(0, nb, chunk):
+        amd.synth_blocks(src[b0:b0 + chunk], n, first + b0, kind)
+        torch.cuda.synchronize()
+        log("[rank %d] synth %d/%d blocks (%.0f s)" % (rank, min(b0 + chunk, nb), nb,
+                                                        time.time() - t0))
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        amd.compress_batch(src, sizes, comp, csz, stream=stream)
+        if ev:
+            ev[1].record(stream)
+        amd.decompress_batch(comp, csz, out, dres, dst_caps=sizes, stream=stream)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- correctness + ratio (outside the timed region) ----
+    ok = bool((dres == n).all().item()) and bool(torch.equal(out, src))
+    comp_bytes = int(csz.to(torch.int64).sum().item())
+    sample_ok = None
+    if rank == 0 and args.verify_sample > 0:
+        try:
+            orc = C.CDLL(os.path.join(ROOT, "oracle", "liblz4_oracle.so"))
+            idx = torch.linspace(0, nb - 1, args.verify_sample).long()
+            cs = csz[idx].cpu().tolist()
+            cb = comp[idx].cpu().numpy()
+            sb = src[idx].cpu().numpy()
+            sample_ok = True
+            for j in range(len(cs)):
+                blk = cb[j, :cs[j]].tobytes()
+                ob = C.create_string_buffer(n + 64)
+                r = orc.orc_decompress_safe(C.create_string_buffer(blk + b"\0" * 16, len(blk) + 16),
+                                            ob, len(blk), n)
+                sample_ok &= (r == n and ob.raw[:n] == sb[j].tobytes())
+        except OSError:
+            sample_ok = None
+    if dist:
+        agg = torch.tensor([comp_bytes, int(ok)], dtype=torch.int64, device="cuda")
+        dist.all_reduce(agg, op=dist.ReduceOp.SUM)
+        comp_bytes, ok = int(agg[0].item()), int(agg[1].item()) == world
+
+    total_bytes = nb * n * world
+    ms_step = elapsed / args.steps * 1e3
+    value = total_bytes / (elapsed / args.steps) / GIB
+    ratio = total_bytes / max(comp_bytes, 1)
+
+    # per-kernel roofline (this rank; algorithmic bytes = n + c per block per kernel)
+    alg = (nb * n + comp_bytes / world)
+    enc_gbps = alg / (enc_ms * 1e-3) / 1e9
+    dec_gbps = alg / (dec_ms * 1e-3) / 1e9
+    dom = "lz4_encode_kernel" if enc_ms >= dec_ms else "lz4_decode_kernel"
+    dom_gbps = enc_gbps if enc_ms >= dec_ms else dec_gbps
+    roof = {"bound": "hbm", "achieved": round(dom_gbps, 1), "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": round(dom_gbps / HBM_PEAK_GBPS, 4),
+            "traffic": pmc_traffic(dom, nb), "kernel": dom,
+            "bytes_per_launch": int(alg),
+            "avg_launch_ms": round(enc_ms if enc_ms >= dec_ms else dec_ms, 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(n, kind, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (SURVEY App. C gen_%s, seed = block id, generated on device)"
+                    % args.kind,
+            "config": {"workload": "%d x %d KiB %s blocks per GPU, compress+decompress"
+                                   % (nb, n >> 10, "compressible" if kind else "random"),
+                       "blocks_per_gpu": nb, "block_bytes": n, "parallelism": "blocks%d" % world},
+            "ratio": round(ratio, 4),
+            "encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3),
+            "encode_GBps": round(enc_gbps, 1), "decode_GBps": round(dec_gbps, 1),
+            "verified": bool(ok), "oracle_sample_ok": sample_ok,
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -21,9 +21,12 @@ def run_encode(torch, amd, srcs, caps=None, in_mis=None, out_mis=None):
     src, sptr, _ = pack(torch, srcs, misalign=in_mis)
     dst, dptr, doffs = alloc_out(torch, caps, misalign=out_mis)
     res = ints(torch, [0] * len(srcs))
+    # keep every tensor referenced until the kernel has run (raw pointers escape
+    # torch's stream-ordered allocator)
+    sizes, capt = ints(torch, map(len, srcs)), ints(torch, caps)
     rc = amd.lib().APE_LZ4_compress_batch_dev(
-        sptr.data_ptr(), ints(torch, map(len, srcs)).data_ptr(), dptr.data_ptr(),
-        ints(torch, caps).data_ptr(), res.data_ptr(), len(srcs), None)
+        sptr.data_ptr(), sizes.data_ptr(), dptr.data_ptr(), capt.data_ptr(), res.data_ptr(),
+        len(srcs), None)
     assert rc == 0, amd.gpu_last_error()
     torch.cuda.synchronize()
     rs = res.cpu().tolist()
