@@ -34,10 +34,8 @@ constexpr int kStage = kChunk + kMargin;
 constexpr int kWalkers = 64;                 // wave 0
 constexpr int kSeg = kChunk / kWalkers;      // 32 compressed bytes per walker
 constexpr int kMaxSeq = kChunk / 3 + 4;      // each non-final sequence >= 3 bytes
-constexpr int kShort = 64;                   // longer copies go to wave 0
 constexpr uint32_t kEnd = 0xFFFFFFFFu;       // "chain ended" exit marker
 
-enum : uint8_t { F_LONGLIT = 1, F_DEFER_MATCH = 2 };
 enum { T_NONE = 0, T_DONE = 1, T_ERR = 2 };
 
 struct SeqDesc {
@@ -50,7 +48,6 @@ struct SeqDesc {
 struct __attribute__((aligned(16))) DecShared {
     uint8_t out[kMaxBlock + 16];
     uint8_t comp[kStage];
-    uint8_t flags[kMaxSeq];
     SeqDesc desc[kMaxSeq];
     uint32_t cbase, out0, nseq, carry, out_next;
     int state, result;
@@ -105,6 +102,47 @@ __device__ uint32_t walk(const DecShared &S, const DecCtx &c, uint32_t cbase, ui
             } while (s == 255);
         }
         nbytes += lit + ml + kMinMatch;
+        t = q;
+    }
+    return t;
+}
+
+// Exit-only walk used by the fixpoint iterations.  `vis` collects the token
+// positions visited (bit t - seg_lo); when a re-walk from a new entry reaches a
+// position the previous walk visited, the rest is identical, so it stops there.
+__device__ uint32_t walk_exit(const DecShared &S, const DecCtx &c, uint32_t cbase, uint32_t t,
+                              uint32_t seg_lo, uint32_t seg_hi, uint32_t prev_vis,
+                              uint32_t prev_ex, uint32_t &vis) {
+    vis = 0;
+    while (t < seg_hi) {
+        const uint32_t bit = 1u << (t - seg_lo);
+        if (prev_vis & bit) {
+            vis |= prev_vis & ~(bit - 1u);
+            return prev_ex;
+        }
+        vis |= bit;
+        if ((int)t >= c.csize) return kEnd;
+        uint32_t tok = rb(S, c, cbase, t);
+        uint32_t ip = t + 1;
+        uint32_t lit = tok >> 4;
+        if (lit == 15) {
+            uint32_t s;
+            do {
+                s = rb(S, c, cbase, ip);
+                ip++;
+                lit += s;
+            } while ((int)ip < c.csize - 15 && s == 255);
+        }
+        if ((int64_t)ip + lit > (int64_t)c.csize - 8) return kEnd;
+        uint32_t q = ip + lit + 2;
+        if ((tok & 15) == 15) {
+            uint32_t s;
+            do {
+                if ((int)q > c.csize - kLastLiterals) return kEnd;
+                s = rb(S, c, cbase, q);
+                q++;
+            } while (s == 255);
+        }
         t = q;
     }
     return t;
@@ -175,10 +213,33 @@ __device__ int validate(DecShared &S, const DecCtx &c, uint32_t cbase, uint32_t 
     return T_NONE;
 }
 
-__device__ __forceinline__ void copy_match_bytes(uint8_t *out, uint32_t ms, uint32_t d,
-                                                 uint32_t ml) {
-    // forward byte copy == LZ4 semantics for overlapping matches
-    for (uint32_t k = 0; k < ml; k++) out[ms + k] = out[ms + k - d];
+// Largest i with desc[i].out <= pos (descriptors are in output order).
+__device__ __forceinline__ uint32_t find_seq(const DecShared &S, uint32_t nseq, uint32_t pos) {
+    uint32_t lo = 0, hi = nseq - 1;
+    while (lo < hi) {
+        uint32_t mid = (lo + hi + 1) >> 1;
+        if (S.desc[mid].out <= pos) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Value of output byte `s` (>= out0, inside this chunk) by walking its source
+// chain back to a literal or to output before the chunk.  Each hop moves to
+// before the current sequence's match start, so it terminates.
+__device__ uint32_t resolve(const DecShared &S, const DecCtx &c, uint32_t cbase, uint32_t nseq,
+                            uint32_t out0, uint32_t s, const uint8_t *out) {
+    for (;;) {
+        const SeqDesc d = S.desc[find_seq(S, nseq, s)];
+        const uint32_t lit_end = d.out + d.lit_len;
+        if (s < lit_end) return rb(S, c, cbase, d.lit_src + (s - d.out));
+        const uint32_t off = d.mo & 0xFFFFu;
+        if (off == 0) return 0;
+        uint32_t k = s - lit_end;
+        if (k >= off) k %= off;
+        s = lit_end - off + k;
+        if (s < out0) return out[s];
+    }
 }
 
 }  // namespace
@@ -230,9 +291,18 @@ lz4_decode_kernel(BlockArgs a) {
         const uint32_t cbase = S.cbase;
         const uint32_t out0 = S.out0;
         // 1. stage
-        for (int i = tid; i < kStage; i += kThreads) {
-            uint32_t p = cbase + i;
-            S.comp[i] = ((int)p < c.csize) ? c.src[p] : 0;
+        {
+            uint8_t v[(kStage + kThreads - 1) / kThreads];
+#pragma unroll
+            for (int j = 0; j < (kStage + kThreads - 1) / kThreads; j++) {
+                uint32_t i = tid + j * kThreads, p = cbase + i;
+                v[j] = (i < (uint32_t)kStage && (int)p < c.csize) ? c.src[p] : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < (kStage + kThreads - 1) / kThreads; j++) {
+                uint32_t i = tid + j * kThreads;
+                if (i < (uint32_t)kStage) S.comp[i] = v[j];
+            }
         }
         __syncthreads();
 
@@ -240,17 +310,30 @@ lz4_decode_kernel(BlockArgs a) {
         if (wave == 0) {
             const uint32_t seg_lo = cbase + lane * kSeg;
             const uint32_t seg_hi = seg_lo + kSeg;
-            uint32_t entry = (lane == 0) ? cbase : seg_lo;
-            uint32_t ex, nseq, nbytes;
+            // On the true chain a walker's entry is the max of all earlier walkers'
+            // exits (chain positions only grow) and never below its segment start.
+            const uint32_t floor_e = seg_lo > cbase ? seg_lo : cbase;
+            uint32_t entry = floor_e, ex = 0, vis = 0, pvis = 0, pex = 0;
             for (int it = 0; it < 2 * kWalkers + 2; it++) {
-                if (entry < seg_hi) ex = walk(S, c, cbase, entry, seg_hi, nseq, nbytes);
-                else { ex = entry; nseq = 0; nbytes = 0; }
-                uint32_t prev = __shfl_up(ex, 1, 64);
-                uint32_t ne = (lane == 0) ? cbase : prev;
+                if (entry < seg_hi) ex = walk_exit(S, c, cbase, entry, seg_lo, seg_hi, pvis, pex, vis);
+                else { ex = entry; vis = 0; }
+                pvis = vis;
+                pex = ex;
+                uint32_t mx = ex;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    uint32_t y = __shfl_up(mx, d, 64);
+                    if (lane >= d) mx = mx > y ? mx : y;
+                }
+                uint32_t prev = __shfl_up(mx, 1, 64);
+                uint32_t ne = (lane == 0 || prev < floor_e) ? floor_e : prev;
                 bool ch = ne != entry;
                 entry = ne;
                 if (!__any(ch)) break;
             }
+            uint32_t nseq = 0, nbytes = 0;
+            if (entry < seg_hi) ex = walk(S, c, cbase, entry, seg_hi, nseq, nbytes);
+            else ex = entry;
             const uint32_t seq0 = wave_excl_scan(nseq);
             const uint32_t byt0 = wave_excl_scan(nbytes);
             uint32_t cnt = 0;
@@ -267,6 +350,7 @@ lz4_decode_kernel(BlockArgs a) {
                     S.nseq = s0;
                     S.state = fterm;
                     S.result = ftv;
+                    S.out_next = (fterm == T_DONE) ? (uint32_t)ftv : out0;
                 }
             } else {
                 uint32_t tot = __shfl(seq0 + nseq, 63, 64);
@@ -283,61 +367,47 @@ lz4_decode_kernel(BlockArgs a) {
         if (S.state == T_ERR) break;
         const uint32_t nseq = S.nseq;
 
-        // 4a. literals and final-source matches, one sequence per thread
-        for (uint32_t i = tid; i < nseq; i += kThreads) {
-            SeqDesc d = S.desc[i];
-            uint8_t f = 0;
-            if (d.lit_len > (uint32_t)kShort) {
-                f |= F_LONGLIT;
-            } else {
-                for (uint32_t k = 0; k < d.lit_len; k++) out[d.out + k] = rb(S, c, cbase, d.lit_src + k);
-            }
-            if (d.mo) {
-                uint32_t off = d.mo & 0xFFFF, ml = d.mo >> 16;
-                uint32_t ms = d.out + d.lit_len;
-                uint32_t src_hi = ms - off + (ml < off ? ml : off);  // exclusive
-                if (src_hi <= out0 && ml <= (uint32_t)kShort) copy_match_bytes(out, ms, off, ml);
-                else f |= F_DEFER_MATCH;
-            }
-            S.flags[i] = f;
-        }
-        __syncthreads();
-
-        // 4b. deferred copies in sequence order, wave 0 cooperatively
-        if (wave == 0) {
-            for (uint32_t base = 0; base < nseq; base += 64) {
-                uint32_t i = base + lane;
-                uint8_t f = (i < nseq) ? S.flags[i] : 0;
-                unsigned long long m = __ballot(f != 0);
-                while (m) {
-                    int l = __ffsll((long long)m) - 1;
-                    m &= m - 1;
-                    SeqDesc d = S.desc[base + l];
-                    uint8_t ff = S.flags[base + l];
-                    if (ff & F_LONGLIT) {
-                        for (uint32_t k = lane; k < d.lit_len; k += 64)
-                            out[d.out + k] = rb(S, c, cbase, d.lit_src + k);
+        // 4. COPY.  Every output byte of this chunk resolves on its own: a literal
+        // byte comes from the compressed stream, a match byte from out[src] when
+        // src precedes the chunk, else by following src's own sequence backwards
+        // until it lands on a literal or on pre-chunk output.  Only final data is
+        // ever read, so there is no ordering and no barrier inside a chunk.
+        {
+            const uint32_t out_end = S.out_next;
+            for (uint32_t base = (out0 & ~15u) + 16u * tid; base < out_end; base += 16u * kThreads) {
+                uint32_t q = base < out0 ? out0 : base;
+                const uint32_t qe = base + 16u < out_end ? base + 16u : out_end;
+                if (q >= qe) continue;
+                uint32_t si = find_seq(S, nseq, q);
+                SeqDesc d = S.desc[si];
+                uint32_t lit_end = d.out + d.lit_len;
+                uint32_t off = d.mo & 0xFFFFu, mend = lit_end + (d.mo >> 16);
+                uint32_t k = 0;
+                bool kvalid = false;
+                for (; q < qe; q++) {
+                    while (q >= mend && si + 1 < nseq) {
+                        d = S.desc[++si];
+                        lit_end = d.out + d.lit_len;
+                        off = d.mo & 0xFFFFu;
+                        mend = lit_end + (d.mo >> 16);
+                        kvalid = false;
                     }
-                    if (ff & F_DEFER_MATCH) {
-                        uint32_t off = d.mo & 0xFFFF, ml = d.mo >> 16;
-                        uint32_t ms = d.out + d.lit_len;
-                        if (off >= 64) {
-                            for (uint32_t k0 = 0; k0 < ml; k0 += 64) {
-                                uint32_t k = k0 + lane;
-                                if (k < ml) out[ms + k] = out[ms + k - off];
-                            }
-                        } else if (off > 0) {
-                            uint32_t r = lane % off, step = 64 % off;
-                            for (uint32_t k0 = 0; k0 < ml; k0 += 64) {
-                                uint32_t k = k0 + lane;
-                                if (k < ml) out[ms + k] = out[ms - off + r];
-                                r += step;
-                                if (r >= off) r -= off;
-                            }
+                    uint32_t v;
+                    if (q < lit_end) {
+                        v = rb(S, c, cbase, d.lit_src + (q - d.out));
+                    } else if (off == 0) {
+                        v = 0;  // offset 0: the reference copies stale dst bytes (App. B)
+                    } else {
+                        if (!kvalid) {
+                            k = q - lit_end;
+                            if (k >= off) k %= off;
+                            kvalid = true;
                         }
-                        // offset 0: output depends on prior dst contents in the
-                        // reference; left as is.
+                        const uint32_t src = lit_end - off + k;
+                        v = (src < out0) ? out[src] : resolve(S, c, cbase, nseq, out0, src, out);
+                        if (++k == off) k = 0;
                     }
+                    out[q] = (uint8_t)v;
                 }
             }
         }

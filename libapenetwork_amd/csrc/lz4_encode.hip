@@ -43,6 +43,7 @@ constexpr int kMaxL = 32;               // per-position match length cap
 constexpr uint32_t kTrunc = 0xFFFFu;    // len field: "longer than kMaxL"
 constexpr int kOutCap = kMaxBlock + kMaxBlock / 255 + 16;  // compressBound(64 KiB)
 constexpr int kLongLit = 64;
+constexpr int kLaneExt = 256;         // lane-serial extension budget in the walk
 
 struct __attribute__((aligned(16))) EncShared {
     uint8_t out[kOutCap + 32];
@@ -245,15 +246,30 @@ lz4_encode_kernel(BlockArgs a) {
                             uint32_t v = S.info[m - R0];
                             uint32_t len = v >> 16;
                             if (len == kTrunc) {
-                                if (trusted) {
+                                // lane-serial extension within a budget; only a
+                                // longer match needs the cooperative path
+                                const uint32_t off = v & 0xFFFFu, lim = mlimit - m;
+                                uint32_t l = kMaxL;
+                                bool exact = false;
+                                while (l < lim && l < (uint32_t)kLaneExt) {
+                                    uint32_t x = ld32(S.in, m + l) ^ ld32(S.in, m - off + l);
+                                    if (x) { l += __builtin_ctz(x) >> 3; exact = true; break; }
+                                    l += 4;
+                                }
+                                if (l >= lim) { l = lim; exact = true; }
+                                if (exact) {
+                                    S.info[m - R0] = off | (l << 16);
+                                    len = l;
+                                } else if (trusted) {
                                     need = true;
                                     nm = m;
-                                    noff = v & 0xFFFFu;
+                                    noff = off;
                                 } else {
                                     unknown = true;
                                     active = false;
                                 }
-                            } else {
+                            }
+                            if (!need && !unknown && len != kTrunc) {
                                 p = m + len;
                                 last_end = p;
                                 active = p < seg_hi;
