@@ -20,7 +20,8 @@ __all__ = [
 ]
 
 _HERE = _os.path.dirname(_os.path.abspath(__file__))
-LIB_PATH = _os.path.join(_HERE, "libape_lz4_amd.so")
+# APE_LZ4_LIB selects the diagnostic phase-timer build (tools/phase_stats.py) only.
+LIB_PATH = _os.environ.get("APE_LZ4_LIB") or _os.path.join(_HERE, "libape_lz4_amd.so")
 MAX_BLOCK = 65536
 ERANGE = -2147483648
 

@@ -9,18 +9,20 @@
 // The compressed stream is processed in chunks of kChunk bytes:
 //  1. stage the chunk (+ margin) into LDS;
 //  2. TOKEN CHAIN: wave 0's 64 lanes each own a 32-byte segment of the chunk and
-//     walk LZ4 tokens from a guessed start (segment start; lane 0 starts at the
-//     exact carried position).  Each lane's exit becomes the next lane's entry
-//     and lanes re-walk until no entry changes -- a fixpoint that equals the
-//     sequential token chain (walks from different starts coalesce quickly, the
-//     "Kruskal count" effect, so this converges in a few rounds);
-//  3. VALIDATE: lanes re-walk their sequences with exact output positions from
-//     a wave prefix-sum, applying the reference's checks in the reference's
-//     order, so errors return the identical -(ip - src) - 1, and emit one
-//     descriptor per sequence;
-//  4. COPY: all 256 threads copy literals, then matches whose source lies in
-//     already-final output; wave 0 then does the remaining (dependent or long)
-//     copies in sequence order.
+//     walk LZ4 tokens from a guessed start.  A walker's entry is the max of the
+//     earlier walkers' exits (chain positions only grow); lanes re-walk until no
+//     entry changes -- a fixpoint equal to the sequential token chain.  Walks
+//     from different starts coalesce quickly ("Kruskal count"), and a re-walk
+//     stops as soon as it reaches a token the previous walk visited;
+//  3. VALIDATE: lanes re-walk their sequences with exact output positions from a
+//     wave prefix-sum, applying the reference's checks in the reference's order,
+//     so errors return the identical -(ip - src) - 1, and emit one descriptor per
+//     sequence;
+//  4. COPY: the 4 waves take 128-byte output steps round-robin.  A byte whose
+//     source lies below the published frontier reads it directly; a source inside
+//     the same step resolves through the step's descriptors (lane shuffles); only
+//     a source in the few steps still in flight waits for the frontier.  The
+//     lowest unfinished step never waits, so the scheme cannot deadlock.
 #include "lz4_gpu_internal.h"
 
 namespace apelz4 {
@@ -30,10 +32,11 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kChunk = 2048;                 // compressed bytes walked per round
 constexpr int kMargin = 320;                 // staged beyond the chunk
-constexpr int kStage = kChunk + kMargin;
+constexpr int kStage = kChunk + kMargin;     // multiple of 4
 constexpr int kWalkers = 64;                 // wave 0
 constexpr int kSeg = kChunk / kWalkers;      // 32 compressed bytes per walker
 constexpr int kMaxSeq = kChunk / 3 + 4;      // each non-final sequence >= 3 bytes
+constexpr int kStep = 128;                   // output bytes per copy step (2 per lane)
 constexpr uint32_t kEnd = 0xFFFFFFFFu;       // "chain ended" exit marker
 
 enum { T_NONE = 0, T_DONE = 1, T_ERR = 2 };
@@ -47,9 +50,9 @@ struct SeqDesc {
 
 struct __attribute__((aligned(16))) DecShared {
     uint8_t out[kMaxBlock + 16];
-    uint8_t comp[kStage];
+    uint32_t comp[kStage / 4 + 2];  // staged compressed bytes, zero beyond the input
     SeqDesc desc[kMaxSeq];
-    uint32_t cbase, out0, nseq, carry, out_next;
+    uint32_t cbase, out0, nseq, carry, out_next, front;
     int state, result;
 };
 
@@ -61,55 +64,51 @@ struct DecCtx {
     bool partial;
 };
 
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
+}
+
 __device__ __forceinline__ uint32_t rb(const DecShared &S, const DecCtx &c, uint32_t cbase,
                                        uint32_t pos) {
     uint32_t r = pos - cbase;
-    if (r < (uint32_t)kStage) return S.comp[r];
+    if (r < (uint32_t)kStage) return (S.comp[r >> 2] >> (8u * (r & 3u))) & 0xFFu;
     return ((int)pos < c.csize) ? (uint32_t)c.src[pos] : 0u;
 }
 
-// Token-chain walk (input side only): from token position t, walk until the
-// next token position is >= seg_hi.  Returns the exit; kEnd when the chain
-// terminates (final literal run or an input-side error) inside this segment.
-__device__ uint32_t walk(const DecShared &S, const DecCtx &c, uint32_t cbase, uint32_t t,
-                         uint32_t seg_hi, uint32_t &nseq, uint32_t &nbytes) {
-    nseq = 0;
-    nbytes = 0;
-    while (t < seg_hi) {
-        if ((int)t >= c.csize) return kEnd;
-        uint32_t tok = rb(S, c, cbase, t);
-        uint32_t ip = t + 1;
-        uint32_t lit = tok >> 4;
-        if (lit == 15) {
-            uint32_t s;
-            do {
-                s = rb(S, c, cbase, ip);
-                ip++;
-                lit += s;
-            } while ((int)ip < c.csize - 15 && s == 255);
-        }
-        nseq++;
-        if ((int64_t)ip + lit > (int64_t)c.csize - 8) return kEnd;
-        uint32_t q = ip + lit + 2;
-        uint32_t ml = tok & 15;
-        if (ml == 15) {
-            uint32_t s;
-            do {
-                if ((int)q > c.csize - kLastLiterals) return kEnd;
-                s = rb(S, c, cbase, q);
-                q++;
-                ml += s;
-            } while (s == 255);
-        }
-        nbytes += lit + ml + kMinMatch;
-        t = q;
+// 4 bytes at pos, little-endian (two aligned LDS dwords in the staged window).
+__device__ __forceinline__ uint32_t rd4(const DecShared &S, const DecCtx &c, uint32_t cbase,
+                                        uint32_t pos) {
+    uint32_t r = pos - cbase;
+    if (r + 4u <= (uint32_t)kStage) return funnel(S.comp[(r >> 2) + 1], S.comp[r >> 2], r & 3u);
+    return rb(S, c, cbase, pos) | (rb(S, c, cbase, pos + 1) << 8) |
+           (rb(S, c, cbase, pos + 2) << 16) | (rb(S, c, cbase, pos + 3) << 24);
+}
+
+// Token and literal length of the sequence at t (:1330-1342): returns the token,
+// sets ip to the first literal byte and lit to the literal length.
+__device__ __forceinline__ uint32_t parse_lit(const DecShared &S, const DecCtx &c,
+                                              uint32_t cbase, uint32_t t, uint32_t &ip,
+                                              uint32_t &lit) {
+    const uint32_t w = rd4(S, c, cbase, t);
+    const uint32_t tok = w & 0xFFu;
+    ip = t + 1;
+    lit = tok >> 4;
+    if (lit == 15) {
+        uint32_t s;
+        do {
+            const uint32_t k = ip - t;
+            s = (k < 4) ? (w >> (8u * k)) & 0xFFu : rb(S, c, cbase, ip);
+            ip++;
+            lit += s;
+        } while ((int)ip < c.csize - 15 && s == 255);
     }
-    return t;
+    return tok;
 }
 
 // Exit-only walk used by the fixpoint iterations.  `vis` collects the token
 // positions visited (bit t - seg_lo); when a re-walk from a new entry reaches a
 // position the previous walk visited, the rest is identical, so it stops there.
+// Returns kEnd when the chain terminates (final literals / input-side error).
 __device__ uint32_t walk_exit(const DecShared &S, const DecCtx &c, uint32_t cbase, uint32_t t,
                               uint32_t seg_lo, uint32_t seg_hi, uint32_t prev_vis,
                               uint32_t prev_ex, uint32_t &vis) {
@@ -122,27 +121,50 @@ __device__ uint32_t walk_exit(const DecShared &S, const DecCtx &c, uint32_t cbas
         }
         vis |= bit;
         if ((int)t >= c.csize) return kEnd;
-        uint32_t tok = rb(S, c, cbase, t);
-        uint32_t ip = t + 1;
-        uint32_t lit = tok >> 4;
-        if (lit == 15) {
-            uint32_t s;
-            do {
-                s = rb(S, c, cbase, ip);
-                ip++;
-                lit += s;
-            } while ((int)ip < c.csize - 15 && s == 255);
-        }
+        uint32_t ip, lit;
+        const uint32_t tok = parse_lit(S, c, cbase, t, ip, lit);
         if ((int64_t)ip + lit > (int64_t)c.csize - 8) return kEnd;
         uint32_t q = ip + lit + 2;
         if ((tok & 15) == 15) {
-            uint32_t s;
+            const uint32_t w = rd4(S, c, cbase, q);
+            uint32_t s, k = 0;
             do {
                 if ((int)q > c.csize - kLastLiterals) return kEnd;
-                s = rb(S, c, cbase, q);
+                s = (k < 4) ? (w >> (8u * k)) & 0xFFu : rb(S, c, cbase, q);
                 q++;
+                k++;
             } while (s == 255);
         }
+        t = q;
+    }
+    return t;
+}
+
+// Counting walk: number of sequences and decoded bytes from t to the segment end.
+__device__ uint32_t walk_count(const DecShared &S, const DecCtx &c, uint32_t cbase, uint32_t t,
+                               uint32_t seg_hi, uint32_t &nseq, uint32_t &nbytes) {
+    nseq = 0;
+    nbytes = 0;
+    while (t < seg_hi) {
+        if ((int)t >= c.csize) return kEnd;
+        uint32_t ip, lit;
+        const uint32_t tok = parse_lit(S, c, cbase, t, ip, lit);
+        nseq++;
+        if ((int64_t)ip + lit > (int64_t)c.csize - 8) return kEnd;
+        uint32_t q = ip + lit + 2;
+        uint32_t ml = tok & 15;
+        if (ml == 15) {
+            const uint32_t w = rd4(S, c, cbase, q);
+            uint32_t s, k = 0;
+            do {
+                if ((int)q > c.csize - kLastLiterals) return kEnd;
+                s = (k < 4) ? (w >> (8u * k)) & 0xFFu : rb(S, c, cbase, q);
+                q++;
+                k++;
+                ml += s;
+            } while (s == 255);
+        }
+        nbytes += lit + ml + kMinMatch;
         t = q;
     }
     return t;
@@ -155,23 +177,14 @@ __device__ int validate(DecShared &S, const DecCtx &c, uint32_t cbase, uint32_t 
                         uint32_t seg_hi, int64_t op, uint32_t di, uint32_t &cnt, int &tv) {
     cnt = 0;
     while (t < seg_hi) {
-        uint32_t tok = rb(S, c, cbase, t);
-        uint32_t ip = t + 1;
-        uint32_t lit = tok >> 4;
-        if (lit == 15) {
-            uint32_t s;
-            do {
-                s = rb(S, c, cbase, ip);
-                ip++;
-                lit += s;
-            } while ((int)ip < c.csize - 15 && s == 255);
-        }
-        int64_t cpy = op + lit;
+        uint32_t ip, lit;
+        const uint32_t tok = parse_lit(S, c, cbase, t, ip, lit);
+        const int64_t cpy = op + lit;
         bool fin = c.partial ? (cpy > c.oexit) : (cpy > (int64_t)c.cap - kMFLimit);
         fin = fin || ((int64_t)ip + lit > (int64_t)c.csize - 8);
         if (fin) {  // :1346-1366
-            bool err = c.partial ? (cpy > c.cap || (int64_t)ip + lit > c.csize)
-                                 : ((int64_t)ip + lit != c.csize || cpy > c.cap);
+            const bool err = c.partial ? (cpy > c.cap || (int64_t)ip + lit > c.csize)
+                                       : ((int64_t)ip + lit != c.csize || cpy > c.cap);
             if (err) { tv = -(int)ip - 1; return T_ERR; }
             if (cpy > kMaxBlock) { tv = kErange; return T_ERR; }
             if (di + cnt < (uint32_t)kMaxSeq) {
@@ -181,23 +194,25 @@ __device__ int validate(DecShared &S, const DecCtx &c, uint32_t cbase, uint32_t 
             tv = (int)cpy;
             return T_DONE;
         }
-        uint32_t lit_src = ip;
+        const uint32_t lit_src = ip;
         ip += lit;
-        uint32_t off = rb(S, c, cbase, ip) | (rb(S, c, cbase, ip + 1) << 8);
+        const uint32_t w = rd4(S, c, cbase, ip);
+        const uint32_t off = w & 0xFFFFu;
         ip += 2;
         if (cpy - (int64_t)off < 0) { tv = -(int)ip - 1; return T_ERR; }  // :1375
         uint32_t ml = tok & 15;
         if (ml == 15) {  // :1380-1390
-            uint32_t s;
+            uint32_t s, k = 2;
             do {
                 if ((int)ip > c.csize - kLastLiterals) { tv = -(int)ip - 1; return T_ERR; }
-                s = rb(S, c, cbase, ip);
+                s = (k < 4) ? (w >> (8u * k)) & 0xFFu : rb(S, c, cbase, ip);
                 ip++;
+                k++;
                 ml += s;
             } while (s == 255);
         }
         ml += kMinMatch;
-        int64_t mend = cpy + ml;
+        const int64_t mend = cpy + ml;
         if (mend > (int64_t)c.cap - kLastLiterals) { tv = -(int)ip - 1; return T_ERR; }  // :1444
         if (mend > kMaxBlock) { tv = kErange; return T_ERR; }
         if (di + cnt < (uint32_t)kMaxSeq) {
@@ -213,36 +228,23 @@ __device__ int validate(DecShared &S, const DecCtx &c, uint32_t cbase, uint32_t 
     return T_NONE;
 }
 
-// Largest i with desc[i].out <= pos (descriptors are in output order).
-__device__ __forceinline__ uint32_t find_seq(const DecShared &S, uint32_t nseq, uint32_t pos) {
-    uint32_t lo = 0, hi = nseq - 1;
-    while (lo < hi) {
-        uint32_t mid = (lo + hi + 1) >> 1;
-        if (S.desc[mid].out <= pos) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
-}
-
-// Value of output byte `s` (>= out0, inside this chunk) by walking its source
-// chain back to a literal or to output before the chunk.  Each hop moves to
-// before the current sequence's match start, so it terminates.
-__device__ uint32_t resolve(const DecShared &S, const DecCtx &c, uint32_t cbase, uint32_t nseq,
-                            uint32_t out0, uint32_t s, const uint8_t *out) {
-    for (;;) {
-        const SeqDesc d = S.desc[find_seq(S, nseq, s)];
-        const uint32_t lit_end = d.out + d.lit_len;
-        if (s < lit_end) return rb(S, c, cbase, d.lit_src + (s - d.out));
-        const uint32_t off = d.mo & 0xFFFFu;
-        if (off == 0) return 0;
-        uint32_t k = s - lit_end;
-        if (k >= off) k %= off;
-        s = lit_end - off + k;
-        if (s < out0) return out[s];
-    }
+__device__ __forceinline__ uint32_t front_load(const DecShared &S) {
+    return __hip_atomic_load(&S.front, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 }  // namespace
+
+#ifdef APE_LZ4_STATS
+__device__ unsigned long long g_dec_stats[16];
+hipError_t dec_stats_read(unsigned long long *out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dec_stats), sizeof(g_dec_stats));
+    if (e == hipSuccess && reset) {
+        unsigned long long z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_dec_stats), z, sizeof(z));
+    }
+    return e;
+}
+#endif
 
 template <bool PARTIAL>
 __global__ void __launch_bounds__(kThreads)
@@ -262,23 +264,20 @@ lz4_decode_kernel(BlockArgs a) {
     c.oexit = PARTIAL ? a.target[b] : 0;
     if (PARTIAL && (int64_t)c.oexit > (int64_t)c.cap - kMFLimit) c.oexit = c.cap - kMFLimit;
 
-    // Special cases of :1316-1318 and the empty-input quirk (reads src[0]).
+    // Special cases of :1316-1318 and the empty-input quirk (the reference reads
+    // src[0] even when compressedSize <= 0).
     if (c.cap == 0 || c.csize <= 0) {
         if (tid == 0) {
             int r;
-            if (c.csize < 0) r = -1;  // reference: negative size -> iend < ip (garbage); see DESIGN
-            else if (c.cap == 0) r = (c.csize == 1 && c.src[0] == 0) ? 0 : -1;
-            else {
-                uint32_t t0 = c.src ? c.src[0] : 0u;
-                r = (t0 >= 0xF0) ? -3 : -2;
-            }
+            if (c.cap == 0) r = (c.csize == 1 && c.src[0] == 0) ? 0 : -1;
+            else r = ((c.src ? c.src[0] : 0u) >= 0xF0) ? -3 : -2;
             a.result[b] = r;
         }
         return;
     }
-    if (c.cap < 0) c.cap = -1;  // every size check then fails like the reference
 
     uint8_t *out = S.out + ((uintptr_t)dst & 15);
+    STATS_DECL
     if (tid == 0) {
         S.cbase = 0;
         S.out0 = 0;
@@ -286,35 +285,46 @@ lz4_decode_kernel(BlockArgs a) {
         S.result = 0;
     }
     __syncthreads();
+    STAT(0);
 
     for (;;) {
         const uint32_t cbase = S.cbase;
         const uint32_t out0 = S.out0;
-        // 1. stage
+        // 1. stage (byte loads, all in flight together)
         {
-            uint8_t v[(kStage + kThreads - 1) / kThreads];
+            constexpr int kPer = (kStage + 8 + 4 * kThreads - 1) / (4 * kThreads);
+            uint32_t v[kPer];
 #pragma unroll
-            for (int j = 0; j < (kStage + kThreads - 1) / kThreads; j++) {
-                uint32_t i = tid + j * kThreads, p = cbase + i;
-                v[j] = (i < (uint32_t)kStage && (int)p < c.csize) ? c.src[p] : 0;
+            for (int j = 0; j < kPer; j++) {
+                const uint32_t i = 4u * (tid + j * kThreads);
+                uint32_t x = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t p = cbase + i + k;
+                    if (i + k < (uint32_t)kStage + 8 && (int)p < c.csize)
+                        x |= (uint32_t)c.src[p] << (8 * k);
+                }
+                v[j] = x;
             }
 #pragma unroll
-            for (int j = 0; j < (kStage + kThreads - 1) / kThreads; j++) {
-                uint32_t i = tid + j * kThreads;
-                if (i < (uint32_t)kStage) S.comp[i] = v[j];
+            for (int j = 0; j < kPer; j++) {
+                const uint32_t i = tid + j * kThreads;
+                if (i < (uint32_t)(kStage / 4 + 2)) S.comp[i] = v[j];
             }
         }
+        if (tid == 0) S.front = out0;
         __syncthreads();
+        STAT(1);
+        STAT_ADD(8, 1);
 
         // 2+3. token chain + validation (wave 0)
         if (wave == 0) {
             const uint32_t seg_lo = cbase + lane * kSeg;
             const uint32_t seg_hi = seg_lo + kSeg;
-            // On the true chain a walker's entry is the max of all earlier walkers'
-            // exits (chain positions only grow) and never below its segment start.
             const uint32_t floor_e = seg_lo > cbase ? seg_lo : cbase;
             uint32_t entry = floor_e, ex = 0, vis = 0, pvis = 0, pex = 0;
-            for (int it = 0; it < 2 * kWalkers + 2; it++) {
+            int it = 0;
+            for (; it < 2 * kWalkers + 2; it++) {
                 if (entry < seg_hi) ex = walk_exit(S, c, cbase, entry, seg_lo, seg_hi, pvis, pex, vis);
                 else { ex = entry; vis = 0; }
                 pvis = vis;
@@ -331,15 +341,19 @@ lz4_decode_kernel(BlockArgs a) {
                 entry = ne;
                 if (!__any(ch)) break;
             }
+            STAT(2);
+            STAT_ADD(5, it + 1);
             uint32_t nseq = 0, nbytes = 0;
-            if (entry < seg_hi) ex = walk(S, c, cbase, entry, seg_hi, nseq, nbytes);
+            if (entry < seg_hi) ex = walk_count(S, c, cbase, entry, seg_hi, nseq, nbytes);
             else ex = entry;
             const uint32_t seq0 = wave_excl_scan(nseq);
             const uint32_t byt0 = wave_excl_scan(nbytes);
+            STAT(3);
             uint32_t cnt = 0;
             int tv = 0, term = T_NONE;
             if (entry < seg_hi)
                 term = validate(S, c, cbase, entry, seg_hi, (int64_t)out0 + byt0, seq0, cnt, tv);
+            STAT(4);
             unsigned long long tm = __ballot(term != T_NONE);
             if (tm) {
                 int first = __ffsll((long long)tm) - 1;
@@ -364,54 +378,99 @@ lz4_decode_kernel(BlockArgs a) {
             }
         }
         __syncthreads();
+        STAT(6);
         if (S.state == T_ERR) break;
         const uint32_t nseq = S.nseq;
 
-        // 4. COPY.  Every output byte of this chunk resolves on its own: a literal
-        // byte comes from the compressed stream, a match byte from out[src] when
-        // src precedes the chunk, else by following src's own sequence backwards
-        // until it lands on a literal or on pre-chunk output.  Only final data is
-        // ever read, so there is no ordering and no barrier inside a chunk.
+        // 4. COPY: round-robin 128-byte steps behind a published frontier.
         {
             const uint32_t out_end = S.out_next;
-            for (uint32_t base = (out0 & ~15u) + 16u * tid; base < out_end; base += 16u * kThreads) {
-                uint32_t q = base < out0 ? out0 : base;
-                const uint32_t qe = base + 16u < out_end ? base + 16u : out_end;
-                if (q >= qe) continue;
-                uint32_t si = find_seq(S, nseq, q);
-                SeqDesc d = S.desc[si];
-                uint32_t lit_end = d.out + d.lit_len;
-                uint32_t off = d.mo & 0xFFFFu, mend = lit_end + (d.mo >> 16);
-                uint32_t k = 0;
-                bool kvalid = false;
-                for (; q < qe; q++) {
-                    while (q >= mend && si + 1 < nseq) {
-                        d = S.desc[++si];
-                        lit_end = d.out + d.lit_len;
-                        off = d.mo & 0xFFFFu;
-                        mend = lit_end + (d.mo >> 16);
-                        kvalid = false;
-                    }
-                    uint32_t v;
-                    if (q < lit_end) {
-                        v = rb(S, c, cbase, d.lit_src + (q - d.out));
-                    } else if (off == 0) {
-                        v = 0;  // offset 0: the reference copies stale dst bytes (App. B)
-                    } else {
-                        if (!kvalid) {
-                            k = q - lit_end;
-                            if (k >= off) k %= off;
-                            kvalid = true;
+            const uint32_t first = out0 / kStep, last = (out_end + kStep - 1) / kStep;
+            uint32_t si0 = 0;  // wave-uniform: last descriptor with out <= step start
+            for (uint32_t st = first + wave; st < last; st += kThreads / 64) {
+                const uint32_t base = st * kStep;
+                const uint32_t lo = base > out0 ? base : out0;
+                const uint32_t hi = base + kStep < out_end ? base + kStep : out_end;
+                for (;;) {  // seek (descriptors sorted by output position)
+                    const uint32_t idx = si0 + lane;
+                    const uint32_t o = idx < nseq ? S.desc[idx].out : 0xFFFFFFFFu;
+                    const unsigned long long m = __ballot(o <= lo);
+                    if (m == ~0ull) { si0 += 64; continue; }
+                    si0 += (uint32_t)__popcll(m) - 1u;
+                    break;
+                }
+                const uint32_t idx = si0 + lane;
+                SeqDesc dl = idx < nseq ? S.desc[idx] : SeqDesc{0u, 0xFFFFFFFFu, 0u, 0u};
+                uint32_t pos[2], val[2], rsrc[2];
+                bool live[2], rd[2], pend[2];
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    const uint32_t q = base + 2u * lane + j;
+                    pos[j] = q;
+                    val[j] = 0;
+                    rsrc[j] = 0;
+                    rd[j] = false;
+                    live[j] = q >= lo && q < hi;
+                    pend[j] = live[j];
+                }
+                for (int hop = 0; hop <= kStep; hop++) {  // uniform: shuffles inside
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const uint32_t p = pos[j];
+                        int ol = 0;
+#pragma unroll
+                        for (int s = 32; s >= 1; s >>= 1) {
+                            const uint32_t o = __shfl(dl.out, ol + s, 64);
+                            if (ol + s < 64 && o <= p) ol += s;
                         }
-                        const uint32_t src = lit_end - off + k;
-                        v = (src < out0) ? out[src] : resolve(S, c, cbase, nseq, out0, src, out);
-                        if (++k == off) k = 0;
+                        const uint32_t o_out = __shfl(dl.out, ol, 64);
+                        const uint32_t o_src = __shfl(dl.lit_src, ol, 64);
+                        const uint32_t o_lit = __shfl(dl.lit_len, ol, 64);
+                        const uint32_t o_mo = __shfl(dl.mo, ol, 64);
+                        if (pend[j]) {
+                            const uint32_t le = o_out + o_lit;
+                            const uint32_t off = o_mo & 0xFFFFu;
+                            if (p < le) {
+                                val[j] = rb(S, c, cbase, o_src + (p - o_out));
+                                pend[j] = false;
+                            } else if (off == 0) {
+                                pend[j] = false;  // offset 0: stale dst bytes in the reference
+                            } else {
+                                uint32_t k = p - le;
+                                if (k >= off) k %= off;
+                                const uint32_t src = le - off + k;
+                                if (src < lo) {
+                                    rsrc[j] = src;
+                                    rd[j] = true;
+                                    pend[j] = false;
+                                } else {
+                                    pos[j] = src;  // in-step source: follow it
+                                }
+                            }
+                        }
                     }
-                    out[q] = (uint8_t)v;
+                    if (!__any(pend[0] || pend[1])) break;
+                }
+                // sources in steps still in flight: wait for the frontier
+                uint32_t f = front_load(S);
+                while (__any((rd[0] && rsrc[0] >= f) || (rd[1] && rsrc[1] >= f))) {
+                    __builtin_amdgcn_s_sleep(1);
+                    f = front_load(S);
+                }
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    if (rd[j]) val[j] = out[rsrc[j]];
+                    if (live[j]) out[base + 2u * lane + j] = (uint8_t)val[j];
+                }
+                // publish this step once every earlier step has been published
+                if (lane == 0) {
+                    while (front_load(S) < lo) __builtin_amdgcn_s_sleep(1);
+                    __hip_atomic_store(&S.front, hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         }
         __syncthreads();
+        STAT(7);
         if (S.state == T_DONE) break;
         if (tid == 0) {
             // the chain always advances (>= 3 bytes per sequence); anything else is
@@ -430,15 +489,19 @@ lz4_decode_kernel(BlockArgs a) {
     // 5. result + flush dst[0:result) with 16-byte stores
     const int res = S.result;
     if (tid == 0) a.result[b] = res;
-    if (S.state != T_DONE || res <= 0) return;
-    const uint32_t n = (uint32_t)res;
-    const uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15);
-    const uint32_t h = head < n ? head : n;
-    if ((uint32_t)tid < h) dst[tid] = out[tid];
-    const uint32_t body = (n - h) & ~15u;
-    for (uint32_t k = h + 16 * tid; k < h + body; k += 16 * kThreads)
-        *(uint4 *)(dst + k) = *(const uint4 *)(out + k);
-    for (uint32_t k = h + body + tid; k < n; k += kThreads) dst[k] = out[k];
+    if (S.state == T_DONE && res > 0) {
+        const uint32_t n = (uint32_t)res;
+        const uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15);
+        const uint32_t h = head < n ? head : n;
+        if ((uint32_t)tid < h) dst[tid] = out[tid];
+        const uint32_t body = (n - h) & ~15u;
+        for (uint32_t k = h + 16 * tid; k < h + body; k += 16 * kThreads)
+            *(uint4 *)(dst + k) = *(const uint4 *)(out + k);
+        for (uint32_t k = h + body + tid; k < n; k += kThreads) dst[k] = out[k];
+    }
+    STAT(9);
+    STAT_ADD(10, 1);
+    STATS_FLUSH(g_dec_stats);
 }
 
 hipError_t launch_decode(const BlockArgs &a, bool partial, hipStream_t s) {

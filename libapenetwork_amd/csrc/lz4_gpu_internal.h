@@ -34,6 +34,22 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
+// ---- diagnostic phase timers (built only into libape_lz4_amd_stats.so) ----
+// Thread 0 of every workgroup accumulates s_memtime cycles per phase and adds them
+// to a per-kernel __device__ array at exit.  Never compiled into the product.
+#ifdef APE_LZ4_STATS
+#define STATS_DECL uint64_t st_t_ = clock64(); uint64_t st_acc_[16] = {0};
+#define STAT(i) do { uint64_t t_ = clock64(); st_acc_[i] += t_ - st_t_; st_t_ = t_; } while (0)
+#define STAT_ADD(i, v) (st_acc_[i] += (uint64_t)(v))
+#define STATS_FLUSH(arr) do { if (threadIdx.x == 0) { _Pragma("unroll") for (int i_ = 0; i_ < 16; i_++) atomicAdd(&(arr)[i_], (unsigned long long)st_acc_[i_]); } } while (0)
+#else
+#define STATS_DECL
+#define STAT(i) do {} while (0)
+#define STAT_ADD(i, v) do {} while (0)
+#define STATS_FLUSH(arr) do {} while (0)
+#endif
+hipError_t stats_read(int which, unsigned long long *out, int reset);
+
 // Launchers (lz4_decode.hip / lz4_encode.hip / lz4_synth.hip).
 struct BlockArgs {
     const char *const *src;   // pointer-array form (nullptr when strided)
