@@ -36,7 +36,7 @@ constexpr int kStage = kChunk + kMargin;     // multiple of 4
 constexpr int kWalkers = 64;                 // wave 0
 constexpr int kSeg = kChunk / kWalkers;      // 32 compressed bytes per walker
 constexpr int kMaxSeq = kChunk / 3 + 4;      // each non-final sequence >= 3 bytes
-constexpr int kStep = 128;                   // output bytes per copy step (2 per lane)
+constexpr int kStep = 256;                   // output bytes per copy step (4 per lane)
 constexpr uint32_t kEnd = 0xFFFFFFFFu;       // "chain ended" exit marker
 
 enum { T_NONE = 0, T_DONE = 1, T_ERR = 2 };
@@ -75,34 +75,79 @@ __device__ __forceinline__ uint32_t rb(const DecShared &S, const DecCtx &c, uint
     return ((int)pos < c.csize) ? (uint32_t)c.src[pos] : 0u;
 }
 
-// 4 bytes at pos, little-endian (two aligned LDS dwords in the staged window).
-__device__ __forceinline__ uint32_t rd4(const DecShared &S, const DecCtx &c, uint32_t cbase,
+// 8 bytes at pos, little-endian (three aligned LDS dwords in the staged window).
+__device__ __forceinline__ uint64_t rd8(const DecShared &S, const DecCtx &c, uint32_t cbase,
                                         uint32_t pos) {
-    uint32_t r = pos - cbase;
-    if (r + 4u <= (uint32_t)kStage) return funnel(S.comp[(r >> 2) + 1], S.comp[r >> 2], r & 3u);
-    return rb(S, c, cbase, pos) | (rb(S, c, cbase, pos + 1) << 8) |
-           (rb(S, c, cbase, pos + 2) << 16) | (rb(S, c, cbase, pos + 3) << 24);
+    const uint32_t r = pos - cbase;
+    if (r + 8u <= (uint32_t)kStage) {
+        const uint32_t *w = &S.comp[r >> 2];
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = r & 3u;
+        return (uint64_t)funnel(w1, w0, sh) | ((uint64_t)funnel(w2, w1, sh) << 32);
+    }
+    uint64_t x = 0;
+    for (int k = 0; k < 8; k++) x |= (uint64_t)rb(S, c, cbase, pos + k) << (8 * k);
+    return x;
 }
 
-// Token and literal length of the sequence at t (:1330-1342): returns the token,
-// sets ip to the first literal byte and lit to the literal length.
-__device__ __forceinline__ uint32_t parse_lit(const DecShared &S, const DecCtx &c,
-                                              uint32_t cbase, uint32_t t, uint32_t &ip,
-                                              uint32_t &lit) {
-    const uint32_t w = rd4(S, c, cbase, t);
-    const uint32_t tok = w & 0xFFu;
-    ip = t + 1;
-    lit = tok >> 4;
+// One parsed sequence, input side only (what :1330-1391 read, in that order).
+struct Tok {
+    uint32_t tok;
+    uint32_t ip;    // first literal byte
+    uint32_t lit;   // literal length
+    uint32_t off;   // match offset (read at ip + lit)
+    uint32_t q;     // position after the match-length bytes (next token)
+    uint32_t ml;    // match length - 4
+    uint32_t qerr;  // where the match-length loop hit the input end (mlerr)
+    bool mlerr;
+};
+
+// Usually one LDS round trip: the 8-byte window at the token covers the token,
+// short literal-length bytes, and for short literal runs the offset too.
+__device__ __forceinline__ Tok parse_seq(const DecShared &S, const DecCtx &c, uint32_t cbase,
+                                         uint32_t t) {
+    Tok r;
+    uint64_t w = rd8(S, c, cbase, t);
+    uint32_t base = t;
+#define WB(pos) ((uint32_t)((pos) - base) < 8u ? (uint32_t)(w >> (8u * ((pos) - base))) & 0xFFu \
+                                                 : rb(S, c, cbase, (pos)))
+    r.tok = (uint32_t)w & 0xFFu;
+    uint32_t ip = t + 1, lit = r.tok >> 4;
     if (lit == 15) {
         uint32_t s;
         do {
-            const uint32_t k = ip - t;
-            s = (k < 4) ? (w >> (8u * k)) & 0xFFu : rb(S, c, cbase, ip);
+            s = WB(ip);
             ip++;
             lit += s;
         } while ((int)ip < c.csize - 15 && s == 255);
     }
-    return tok;
+    r.ip = ip;
+    r.lit = lit;
+    const uint32_t qo = ip + lit;
+    if ((uint32_t)(qo - t) > 4u) {  // offset (+2 length bytes) not in the first window
+        w = rd8(S, c, cbase, qo);
+        base = qo;
+    }
+    r.off = WB(qo) | (WB(qo + 1) << 8);
+    uint32_t q = qo + 2, ml = r.tok & 15;
+    r.mlerr = false;
+    r.qerr = 0;
+    if (ml == 15) {
+        uint32_t s;
+        do {
+            if ((int)q > c.csize - kLastLiterals) {
+                r.mlerr = true;
+                r.qerr = q;
+                break;
+            }
+            s = WB(q);
+            q++;
+            ml += s;
+        } while (s == 255);
+    }
+#undef WB
+    r.q = q;
+    r.ml = ml;
+    return r;
 }
 
 // Exit-only walk used by the fixpoint iterations.  `vis` collects the token
@@ -121,21 +166,9 @@ __device__ uint32_t walk_exit(const DecShared &S, const DecCtx &c, uint32_t cbas
         }
         vis |= bit;
         if ((int)t >= c.csize) return kEnd;
-        uint32_t ip, lit;
-        const uint32_t tok = parse_lit(S, c, cbase, t, ip, lit);
-        if ((int64_t)ip + lit > (int64_t)c.csize - 8) return kEnd;
-        uint32_t q = ip + lit + 2;
-        if ((tok & 15) == 15) {
-            const uint32_t w = rd4(S, c, cbase, q);
-            uint32_t s, k = 0;
-            do {
-                if ((int)q > c.csize - kLastLiterals) return kEnd;
-                s = (k < 4) ? (w >> (8u * k)) & 0xFFu : rb(S, c, cbase, q);
-                q++;
-                k++;
-            } while (s == 255);
-        }
-        t = q;
+        const Tok r = parse_seq(S, c, cbase, t);
+        if ((int64_t)r.ip + r.lit > (int64_t)c.csize - 8 || r.mlerr) return kEnd;
+        t = r.q;
     }
     return t;
 }
@@ -147,83 +180,54 @@ __device__ uint32_t walk_count(const DecShared &S, const DecCtx &c, uint32_t cba
     nbytes = 0;
     while (t < seg_hi) {
         if ((int)t >= c.csize) return kEnd;
-        uint32_t ip, lit;
-        const uint32_t tok = parse_lit(S, c, cbase, t, ip, lit);
+        const Tok r = parse_seq(S, c, cbase, t);
         nseq++;
-        if ((int64_t)ip + lit > (int64_t)c.csize - 8) return kEnd;
-        uint32_t q = ip + lit + 2;
-        uint32_t ml = tok & 15;
-        if (ml == 15) {
-            const uint32_t w = rd4(S, c, cbase, q);
-            uint32_t s, k = 0;
-            do {
-                if ((int)q > c.csize - kLastLiterals) return kEnd;
-                s = (k < 4) ? (w >> (8u * k)) & 0xFFu : rb(S, c, cbase, q);
-                q++;
-                k++;
-                ml += s;
-            } while (s == 255);
-        }
-        nbytes += lit + ml + kMinMatch;
-        t = q;
+        if ((int64_t)r.ip + r.lit > (int64_t)c.csize - 8 || r.mlerr) return kEnd;
+        nbytes += r.lit + r.ml + kMinMatch;
+        t = r.q;
     }
     return t;
 }
 
 // Validation walk: the reference's sequence loop (:1324-1458) with exact `op`,
-// emitting descriptors.  Returns T_NONE / T_DONE / T_ERR with `tv` the block
-// result (decoded size, or -(ip)-1, or kErange).
+// checks in the reference's order, emitting descriptors.  Returns T_NONE /
+// T_DONE / T_ERR with `tv` the block result (decoded size, -(ip)-1, or kErange).
 __device__ int validate(DecShared &S, const DecCtx &c, uint32_t cbase, uint32_t t,
                         uint32_t seg_hi, int64_t op, uint32_t di, uint32_t &cnt, int &tv) {
     cnt = 0;
     while (t < seg_hi) {
-        uint32_t ip, lit;
-        const uint32_t tok = parse_lit(S, c, cbase, t, ip, lit);
-        const int64_t cpy = op + lit;
+        const Tok r = parse_seq(S, c, cbase, t);
+        const int64_t cpy = op + r.lit;
         bool fin = c.partial ? (cpy > c.oexit) : (cpy > (int64_t)c.cap - kMFLimit);
-        fin = fin || ((int64_t)ip + lit > (int64_t)c.csize - 8);
+        fin = fin || ((int64_t)r.ip + r.lit > (int64_t)c.csize - 8);
         if (fin) {  // :1346-1366
-            const bool err = c.partial ? (cpy > c.cap || (int64_t)ip + lit > c.csize)
-                                       : ((int64_t)ip + lit != c.csize || cpy > c.cap);
-            if (err) { tv = -(int)ip - 1; return T_ERR; }
+            const bool err = c.partial ? (cpy > c.cap || (int64_t)r.ip + r.lit > c.csize)
+                                       : ((int64_t)r.ip + r.lit != c.csize || cpy > c.cap);
+            if (err) { tv = -(int)r.ip - 1; return T_ERR; }
             if (cpy > kMaxBlock) { tv = kErange; return T_ERR; }
             if (di + cnt < (uint32_t)kMaxSeq) {
-                S.desc[di + cnt] = SeqDesc{ip, (uint32_t)op, lit, 0u};
+                S.desc[di + cnt] = SeqDesc{r.ip, (uint32_t)op, r.lit, 0u};
                 cnt++;
             }
             tv = (int)cpy;
             return T_DONE;
         }
-        const uint32_t lit_src = ip;
-        ip += lit;
-        const uint32_t w = rd4(S, c, cbase, ip);
-        const uint32_t off = w & 0xFFFFu;
-        ip += 2;
-        if (cpy - (int64_t)off < 0) { tv = -(int)ip - 1; return T_ERR; }  // :1375
-        uint32_t ml = tok & 15;
-        if (ml == 15) {  // :1380-1390
-            uint32_t s, k = 2;
-            do {
-                if ((int)ip > c.csize - kLastLiterals) { tv = -(int)ip - 1; return T_ERR; }
-                s = (k < 4) ? (w >> (8u * k)) & 0xFFu : rb(S, c, cbase, ip);
-                ip++;
-                k++;
-                ml += s;
-            } while (s == 255);
-        }
-        ml += kMinMatch;
+        const uint32_t ip_off = r.ip + r.lit + 2;
+        if (cpy - (int64_t)r.off < 0) { tv = -(int)ip_off - 1; return T_ERR; }  // :1375
+        if (r.mlerr) { tv = -(int)r.qerr - 1; return T_ERR; }                   // :1383
+        const uint32_t ml = r.ml + kMinMatch;
         const int64_t mend = cpy + ml;
-        if (mend > (int64_t)c.cap - kLastLiterals) { tv = -(int)ip - 1; return T_ERR; }  // :1444
+        if (mend > (int64_t)c.cap - kLastLiterals) { tv = -(int)r.q - 1; return T_ERR; }  // :1444
         if (mend > kMaxBlock) { tv = kErange; return T_ERR; }
         if (di + cnt < (uint32_t)kMaxSeq) {
-            S.desc[di + cnt] = SeqDesc{lit_src, (uint32_t)op, lit, off | (ml << 16)};
+            S.desc[di + cnt] = SeqDesc{r.ip, (uint32_t)op, r.lit, r.off | (ml << 16)};
             cnt++;
         } else {
             tv = kErange;  // cannot happen for a converged chain (>= 3 bytes/sequence)
             return T_ERR;
         }
         op = mend;
-        t = ip;
+        t = r.q;
     }
     return T_NONE;
 }
@@ -232,6 +236,133 @@ __device__ __forceinline__ uint32_t front_load(const DecShared &S) {
     return __hip_atomic_load(&S.front, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+
+// Last descriptor with out <= pos, searching forward from si0 (wave-uniform).
+__device__ __forceinline__ uint32_t seek(const DecShared &S, uint32_t nseq, uint32_t si0,
+                                         uint32_t pos, int lane) {
+    for (;;) {
+        const uint32_t idx = si0 + lane;
+        const uint32_t o = idx < nseq ? S.desc[idx].out : 0xFFFFFFFFu;
+        const unsigned long long m = __ballot(o <= pos);
+        if (m == ~0ull) { si0 += 64; continue; }
+        return si0 + (uint32_t)__popcll(m) - 1u;
+    }
+}
+
+// Copy output bytes [lo, hi) of the step at `base` (BPL bytes per lane); the 64
+// lanes hold the descriptors si0 .. si0+63, which cover the whole step.
+template <int BPL>
+__device__ __forceinline__ void copy_step(DecShared &S, const DecCtx &c, uint32_t cbase,
+                                          uint32_t nseq, uint32_t si0, uint32_t base,
+                                          uint32_t lo, uint32_t hi, uint8_t *out, int lane) {
+    const uint32_t idx = si0 + lane;
+    const SeqDesc dl = idx < nseq ? S.desc[idx] : SeqDesc{0u, 0xFFFFFFFFu, 0u, 0u};
+    uint32_t pos[BPL], val[BPL], rsrc[BPL];
+    bool live[BPL], rd[BPL], pend[BPL];
+#pragma unroll
+    for (int j = 0; j < BPL; j++) {
+        const uint32_t q = base + BPL * (uint32_t)lane + j;
+        pos[j] = q;
+        val[j] = 0;
+        rsrc[j] = 0;
+        rd[j] = false;
+        live[j] = q >= lo && q < hi;
+        pend[j] = live[j];
+    }
+    // Resolve byte p inside descriptor d: literal -> value, match -> its source;
+    // a source inside this step stays pending (pos = source) for the next hop.
+    auto resolve = [&](int j, uint32_t p, uint32_t d_out, uint32_t d_src, uint32_t d_lit,
+                       uint32_t d_mo) {
+        const uint32_t le = d_out + d_lit;
+        const uint32_t off = d_mo & 0xFFFFu;
+        if (p < le) {
+            val[j] = rb(S, c, cbase, d_src + (p - d_out));
+            pend[j] = false;
+        } else if (off == 0) {
+            pend[j] = false;  // offset 0: stale dst bytes in the reference (App. B)
+        } else {
+            uint32_t k = p - le;
+            if (k >= off) k %= off;
+            const uint32_t src = le - off + k;
+            if (src < lo) {
+                rsrc[j] = src;
+                rd[j] = true;
+                pend[j] = false;
+            } else {
+                pos[j] = src;
+            }
+        }
+    };
+    auto owner = [&](uint32_t p) {
+        int ol = 0;
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) {
+            const uint32_t o = __shfl(dl.out, ol + s, 64);
+            if (ol + s < 64 && o <= p) ol += s;
+        }
+        return ol;
+    };
+    {   // first pass: the lane's BPL consecutive bytes lie in the owner A of the
+        // first one or in its successor B (every non-final sequence is >= 4 bytes)
+        const int ol = owner(base + BPL * (uint32_t)lane);
+        const int ob = ol + 1 < 64 ? ol + 1 : 63;
+        const uint32_t a_out = __shfl(dl.out, ol, 64), a_src = __shfl(dl.lit_src, ol, 64);
+        const uint32_t a_lit = __shfl(dl.lit_len, ol, 64), a_mo = __shfl(dl.mo, ol, 64);
+        const uint32_t b_out = __shfl(dl.out, ob, 64), b_src = __shfl(dl.lit_src, ob, 64);
+        const uint32_t b_lit = __shfl(dl.lit_len, ob, 64), b_mo = __shfl(dl.mo, ob, 64);
+#pragma unroll
+        for (int j = 0; j < BPL; j++) {
+            if (!pend[j]) continue;
+            const uint32_t p = pos[j];
+            if (p < b_out) resolve(j, p, a_out, a_src, a_lit, a_mo);
+            else resolve(j, p, b_out, b_src, b_lit, b_mo);
+        }
+    }
+    // in-step sources (rare): one pending byte per lane per hop
+    for (int hop = 0; hop < BPL * kStep; hop++) {
+        bool any = false;
+        int jj = 0;
+        uint32_t p = 0;
+#pragma unroll
+        for (int j = BPL - 1; j >= 0; j--)
+            if (pend[j]) { any = true; jj = j; p = pos[j]; }
+        if (!__any(any)) break;
+        const int ol = owner(p);
+        const uint32_t d_out = __shfl(dl.out, ol, 64), d_src = __shfl(dl.lit_src, ol, 64);
+        const uint32_t d_lit = __shfl(dl.lit_len, ol, 64), d_mo = __shfl(dl.mo, ol, 64);
+        if (any) {
+#pragma unroll
+            for (int j = 0; j < BPL; j++)
+                if (j == jj) resolve(j, p, d_out, d_src, d_lit, d_mo);
+        }
+    }
+    // sources in steps still in flight: wait for the frontier
+    uint32_t f = front_load(S);
+    for (;;) {
+        bool w = false;
+#pragma unroll
+        for (int j = 0; j < BPL; j++) w |= rd[j] && rsrc[j] >= f;
+        if (!__any(w)) break;
+        __builtin_amdgcn_s_sleep(1);
+        f = front_load(S);
+    }
+    uint32_t word = 0;
+    bool all_live = true;
+#pragma unroll
+    for (int j = 0; j < BPL; j++) {
+        if (rd[j]) val[j] = out[rsrc[j]];
+        word |= (val[j] & 0xFFu) << (8 * j);
+        all_live &= live[j];
+    }
+    uint8_t *o = out + base + BPL * (uint32_t)lane;
+    if (BPL == 4 && all_live && (((uintptr_t)o) & 3) == 0) {
+        *(uint32_t *)o = word;
+    } else {
+#pragma unroll
+        for (int j = 0; j < BPL; j++)
+            if (live[j]) o[j] = (uint8_t)val[j];
+    }
+}
 }  // namespace
 
 #ifdef APE_LZ4_STATS
@@ -329,14 +460,8 @@ lz4_decode_kernel(BlockArgs a) {
                 else { ex = entry; vis = 0; }
                 pvis = vis;
                 pex = ex;
-                uint32_t mx = ex;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    uint32_t y = __shfl_up(mx, d, 64);
-                    if (lane >= d) mx = mx > y ? mx : y;
-                }
-                uint32_t prev = __shfl_up(mx, 1, 64);
-                uint32_t ne = (lane == 0 || prev < floor_e) ? floor_e : prev;
+                const uint32_t prev = wave_shr1(wave_incl_max(ex), 0u);
+                const uint32_t ne = prev < floor_e ? floor_e : prev;
                 bool ch = ne != entry;
                 entry = ne;
                 if (!__any(ch)) break;
@@ -357,9 +482,9 @@ lz4_decode_kernel(BlockArgs a) {
             unsigned long long tm = __ballot(term != T_NONE);
             if (tm) {
                 int first = __ffsll((long long)tm) - 1;
-                uint32_t s0 = __shfl(seq0 + cnt, first, 64);
-                int ftv = __shfl(tv, first, 64);
-                int fterm = __shfl(term, first, 64);
+                uint32_t s0 = lane_val(seq0 + cnt, first);
+                int ftv = (int)lane_val((uint32_t)tv, first);
+                int fterm = (int)lane_val((uint32_t)term, first);
                 if (lane == 0) {
                     S.nseq = s0;
                     S.state = fterm;
@@ -367,9 +492,9 @@ lz4_decode_kernel(BlockArgs a) {
                     S.out_next = (fterm == T_DONE) ? (uint32_t)ftv : out0;
                 }
             } else {
-                uint32_t tot = __shfl(seq0 + nseq, 63, 64);
-                uint32_t last_ex = __shfl(ex, 63, 64);
-                uint32_t tb = __shfl(byt0 + nbytes, 63, 64);
+                uint32_t tot = lane_val(seq0 + nseq, 63);
+                uint32_t last_ex = lane_val(ex, 63);
+                uint32_t tb = lane_val(byt0 + nbytes, 63);
                 if (lane == 0) {
                     S.nseq = tot;
                     S.carry = last_ex;
@@ -382,7 +507,7 @@ lz4_decode_kernel(BlockArgs a) {
         if (S.state == T_ERR) break;
         const uint32_t nseq = S.nseq;
 
-        // 4. COPY: round-robin 128-byte steps behind a published frontier.
+        // 4. COPY: round-robin steps behind a published frontier.
         {
             const uint32_t out_end = S.out_next;
             const uint32_t first = out0 / kStep, last = (out_end + kStep - 1) / kStep;
@@ -391,76 +516,19 @@ lz4_decode_kernel(BlockArgs a) {
                 const uint32_t base = st * kStep;
                 const uint32_t lo = base > out0 ? base : out0;
                 const uint32_t hi = base + kStep < out_end ? base + kStep : out_end;
-                for (;;) {  // seek (descriptors sorted by output position)
-                    const uint32_t idx = si0 + lane;
-                    const uint32_t o = idx < nseq ? S.desc[idx].out : 0xFFFFFFFFu;
-                    const unsigned long long m = __ballot(o <= lo);
-                    if (m == ~0ull) { si0 += 64; continue; }
-                    si0 += (uint32_t)__popcll(m) - 1u;
-                    break;
-                }
-                const uint32_t idx = si0 + lane;
-                SeqDesc dl = idx < nseq ? S.desc[idx] : SeqDesc{0u, 0xFFFFFFFFu, 0u, 0u};
-                uint32_t pos[2], val[2], rsrc[2];
-                bool live[2], rd[2], pend[2];
-#pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    const uint32_t q = base + 2u * lane + j;
-                    pos[j] = q;
-                    val[j] = 0;
-                    rsrc[j] = 0;
-                    rd[j] = false;
-                    live[j] = q >= lo && q < hi;
-                    pend[j] = live[j];
-                }
-                for (int hop = 0; hop <= kStep; hop++) {  // uniform: shuffles inside
-#pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        const uint32_t p = pos[j];
-                        int ol = 0;
-#pragma unroll
-                        for (int s = 32; s >= 1; s >>= 1) {
-                            const uint32_t o = __shfl(dl.out, ol + s, 64);
-                            if (ol + s < 64 && o <= p) ol += s;
-                        }
-                        const uint32_t o_out = __shfl(dl.out, ol, 64);
-                        const uint32_t o_src = __shfl(dl.lit_src, ol, 64);
-                        const uint32_t o_lit = __shfl(dl.lit_len, ol, 64);
-                        const uint32_t o_mo = __shfl(dl.mo, ol, 64);
-                        if (pend[j]) {
-                            const uint32_t le = o_out + o_lit;
-                            const uint32_t off = o_mo & 0xFFFFu;
-                            if (p < le) {
-                                val[j] = rb(S, c, cbase, o_src + (p - o_out));
-                                pend[j] = false;
-                            } else if (off == 0) {
-                                pend[j] = false;  // offset 0: stale dst bytes in the reference
-                            } else {
-                                uint32_t k = p - le;
-                                if (k >= off) k %= off;
-                                const uint32_t src = le - off + k;
-                                if (src < lo) {
-                                    rsrc[j] = src;
-                                    rd[j] = true;
-                                    pend[j] = false;
-                                } else {
-                                    pos[j] = src;  // in-step source: follow it
-                                }
-                            }
-                        }
+                si0 = seek(S, nseq, si0, lo, lane);
+                // 4 bytes per lane; a step that overlaps more than 64 sequences
+                // (all of them ~4 bytes long) is done as two 2-byte-per-lane halves
+                const uint32_t i63 = si0 + 63;
+                if (i63 >= nseq || S.desc[i63].out >= hi) {
+                    copy_step<4>(S, c, cbase, nseq, si0, base, lo, hi, out, lane);
+                } else {
+                    const uint32_t mid = base + kStep / 2;
+                    copy_step<2>(S, c, cbase, nseq, si0, base, lo, mid < hi ? mid : hi, out, lane);
+                    if (mid < hi) {
+                        si0 = seek(S, nseq, si0, mid, lane);
+                        copy_step<2>(S, c, cbase, nseq, si0, mid, mid, hi, out, lane);
                     }
-                    if (!__any(pend[0] || pend[1])) break;
-                }
-                // sources in steps still in flight: wait for the frontier
-                uint32_t f = front_load(S);
-                while (__any((rd[0] && rsrc[0] >= f) || (rd[1] && rsrc[1] >= f))) {
-                    __builtin_amdgcn_s_sleep(1);
-                    f = front_load(S);
-                }
-#pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    if (rd[j]) val[j] = out[rsrc[j]];
-                    if (live[j]) out[base + 2u * lane + j] = (uint8_t)val[j];
                 }
                 // publish this step once every earlier step has been published
                 if (lane == 0) {

@@ -11,8 +11,8 @@
 //   in[64 KiB]     the input block
 //   E[4096]        hash table, u32 = (latest position of earlier rounds) << 16
 //                  | (earliest position of the current round, 0xFFFF = none)
-//   info[2048]     per position of the current round: the two verified candidate
-//                  offsets, replaced by (offset | length << 16) once resolved
+//   info[2048]     per position of the current round: best match (offset |
+//                  length << 16), length 0xFFFF = "at least kEager, extend on use"
 //   out[~64.3 KiB] the compressed block, flushed to HBM with 16-byte stores.
 // The block is processed in rounds of kRound = 2048 positions:
 //   A. every position hashes its 5 bytes (the reference's 64-bit hash,
@@ -20,13 +20,14 @@
 //   B. every position reads E[h]: candidate T (latest earlier-round position)
 //      and L (earliest same-round position, if before it);
 //   C. atomicMax rolls E[h] to (latest position of this round) | 0xFFFF; each
-//      position verifies both candidates' first 4 bytes (no length yet);
+//      position verifies both candidates and measures them up to kEager bytes
+//      with independent 8-byte LDS compares (all loads in flight at once);
 //   D. wave 0 runs the greedy parse: 64 walkers each own 32 positions, jump
-//      match-to-match through a per-segment "has match" bitmask, measure the
-//      match they land on (lazily; cached), and iterate to the fixpoint where
-//      every walker's entry equals the chain position reaching it (identical to
-//      a sequential greedy parse from position 0);
-//   E. wave 0 prefix-sums sequence sizes and emits tokens/literals/offsets.
+//      match-to-match through a per-segment "has match" bitmask, and iterate to
+//      the fixpoint where every walker's entry equals the chain position reaching
+//      it (identical to a sequential greedy parse from position 0); DPP scans
+//      give entries, anchors and output offsets;
+//   E. all 8 waves emit: 8 threads per walker segment, one sequence each.
 // Atomic min/max make the table state independent of thread timing, so the
 // output is a deterministic function of the input.
 #include "lz4_gpu_internal.h"
@@ -43,14 +44,16 @@ constexpr int kSegE = 32;               // positions per walker segment
 constexpr int kOutCap = kMaxBlock + kMaxBlock / 255 + 16;  // compressBound(64 KiB)
 constexpr int kLongLit = 64;
 constexpr uint32_t kLaneExt = 256;      // lane-serial match measuring budget (bytes)
+constexpr uint32_t kEager = 36;         // phase C measures matches up to this length
+constexpr uint32_t kTrunc = 0xFFFFu;    // info length field: "at least kEager"
 
 struct __attribute__((aligned(16))) EncShared {
     uint8_t out[kOutCap + 32];
-    uint8_t in[kMaxBlock + 32];
+    uint8_t in[kMaxBlock + 64];
     uint32_t E[kHashSize];
     uint32_t info[kRound];
     uint32_t mask[kRound / kSegE];
-    uint32_t dl_src[64], dl_dst[64], dl_len[64];  // deferred long literal runs
+    uint32_t seg_entry[64], seg_anchor[64], seg_out[64];  // walker results for emission
     uint32_t carry_p, carry_a, cursor;
     int overflow;
 };
@@ -63,6 +66,26 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh
 __device__ __forceinline__ uint32_t ld32(const uint8_t *in, uint32_t pos) {
     const uint32_t *w = (const uint32_t *)(in + (pos & ~3u));
     return funnel(w[1], w[0], pos & 3u);
+}
+
+// 8 bytes at pos (three aligned LDS dwords)
+__device__ __forceinline__ uint64_t ld64(const uint8_t *in, uint32_t pos) {
+    const uint32_t *w = (const uint32_t *)(in + (pos & ~3u));
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = pos & 3u;
+    return (uint64_t)funnel(w1, w0, sh) | ((uint64_t)funnel(w2, w1, sh) << 32);
+}
+
+// Common-prefix length (from byte 4 on) of positions p and c, up to kEager;
+// the four 8-byte compares are independent loads, so they are all in flight.
+__device__ __forceinline__ uint32_t eager_len(const uint8_t *in, uint32_t p, uint32_t c) {
+    uint64_t x[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) x[s] = ld64(in, p + 4 + 8 * s) ^ ld64(in, c + 4 + 8 * s);
+    uint32_t len = kEager;
+#pragma unroll
+    for (int s = 3; s >= 0; s--)
+        if (x[s]) len = 4 + 8 * s + (__builtin_ctzll(x[s]) >> 3);
+    return len;
 }
 
 __device__ __forceinline__ uint32_t hash5(uint32_t lo32, uint32_t b4) {
@@ -149,7 +172,7 @@ lz4_encode_kernel(BlockArgs a) {
     } else {
         for (int k = tid; k < n; k += kThreads) S.in[k] = src[k];
     }
-    if (tid < 32) S.in[n + tid] = 0;
+    if (tid < 64) S.in[n + tid] = 0;
     for (int i = tid; i < kHashSize; i += kThreads) S.E[i] = 0x0000FFFFu;
     if (tid == 0) {
         S.carry_p = 0;
@@ -208,14 +231,26 @@ lz4_encode_kernel(BlockArgs a) {
         for (int j = 0; j < 4; j++) {
             uint32_t p = p0 + j;
             if (any_hash && p <= hash_end) atomicMax(&S.E[h[j]], (p << 16) | 0xFFFFu);
-            uint32_t cand = 0;
+            uint32_t best = 0;
             if (p >= 1 && p <= mstart_end && n >= 13 && p >= carry_now) {
                 const bool okT = cT[j] < p && ld32(S.in, cT[j]) == lo32[j];
                 const bool okL = cL[j] < p && cL[j] != cT[j] && ld32(S.in, cL[j]) == lo32[j];
-                cand = (okT ? p - cT[j] : 0u) | ((okL ? p - cL[j] : 0u) << 16);
-                if (cand) nib |= 1u << j;
+                const uint32_t lim = mlimit - p;
+                // measure both (independent loads), keep the longer, then the closer
+                uint32_t lT = okT ? eager_len(S.in, p, cT[j]) : 0u;
+                uint32_t lL = okL ? eager_len(S.in, p, cL[j]) : 0u;
+                if (lT > lim) lT = lim;
+                if (lL > lim) lL = lim;
+                const bool pickL = okL && (!okT || lL > lT || (lL == lT && cL[j] > cT[j]));
+                const uint32_t len = pickL ? lL : lT;
+                if (okT || okL) {
+                    const uint32_t off = p - (pickL ? cL[j] : cT[j]);
+                    // a match that reached kEager before the limit may be longer
+                    best = off | ((len >= kEager && len < lim ? kTrunc : len) << 16);
+                    nib |= 1u << j;
+                }
             }
-            S.info[p - R0] = cand;
+            S.info[p - R0] = best;
         }
         if (nib) atomicOr(&S.mask[(4 * tid) / kSegE], nib << ((4 * tid) % kSegE));
         __syncthreads();
@@ -223,17 +258,19 @@ lz4_encode_kernel(BlockArgs a) {
 
         // ---- D/E: greedy parse and emission (wave 0); skipped when the carried
         // match covers the whole round ----
-        if (wave == 0 && carry_now < R0 + kRound) {
+        const bool parse_round = carry_now < R0 + kRound;
+        if (wave == 0 && parse_round) {
             const uint32_t seg_lo = R0 + lane * kSegE;
             const uint32_t seg_hi = seg_lo + kSegE;
             const uint32_t carry = carry_now;
             const uint32_t mword = S.mask[lane];
-            uint32_t rmask = 0;  // my positions whose info holds (offset | length << 16)
             // Entries are lower-bounded by max(seg_lo, carry) and, on the true chain,
             // equal the max of all earlier walkers' exits (chain positions only grow).
             const uint32_t floor_e = seg_lo > carry ? seg_lo : carry;
             uint32_t entry = floor_e;
             uint32_t ex = 0, last_end = 0;  // last_end: end of my last match, 0 = none
+            uint32_t first_m = 0, rest = 0; // first match start; bytes of my sequences
+                                            // except the first one's literal run
             int conf = 1;                   // walkers [0, conf) have exact entries
             int it_done = 0;
             (void)it_done;
@@ -244,8 +281,10 @@ lz4_encode_kernel(BlockArgs a) {
                 const bool trusted = lane < conf;
                 uint32_t p = entry;
                 last_end = 0;
+                first_m = 0xFFFFFFFFu;
+                rest = 0;
                 bool active = p < seg_hi, need = false, unknown = false;
-                uint32_t nm = 0, noff = 0, nlen = 0;
+                uint32_t nm = 0, noff = 0;
                 while (__any(active)) {
                     if (active && !need) {
                         const uint32_t w = mword & (0xFFFFFFFFu << (p - seg_lo));
@@ -254,71 +293,79 @@ lz4_encode_kernel(BlockArgs a) {
                             active = false;
                         } else {
                             const uint32_t m = seg_lo + __builtin_ctz(w);
-                            const uint32_t bit = 1u << (m - seg_lo);
                             const uint32_t v = S.info[m - R0];
-                            uint32_t len = 0;
-                            if (rmask & bit) {
-                                len = v >> 16;
-                            } else {
-                                // measure both candidates; keep the longer (then closer)
-                                const uint32_t lim = mlimit - m;
-                                const uint32_t oT = v & 0xFFFFu, oL = v >> 16;
-                                bool xT = true, xL = true;
-                                const uint32_t lT = oT ? measure(S.in, m, oT, lim, xT) : 0;
-                                const uint32_t lL = oL ? measure(S.in, m, oL, lim, xL) : 0;
-                                // an inexact length is >= kLaneExt > any exact one below it
-                                const uint32_t kT = xT ? lT : 0x10000u, kL = xL ? lL : 0x10000u;
-                                const bool pickL = oL && (!oT || kL > kT || (kL == kT && oL < oT));
-                                const uint32_t off = pickL ? oL : oT;
-                                const bool exact = pickL ? xL : xT;
-                                len = pickL ? lL : lT;
+                            uint32_t len = v >> 16;
+                            if (len == kTrunc) {
+                                // lane-serial extension within a budget; only a
+                                // longer match needs the cooperative path
+                                const uint32_t off = v & 0xFFFFu, lim = mlimit - m;
+                                uint32_t l = kEager;
+                                bool exact = false;
+                                while (l < lim && l < kLaneExt) {
+                                    const uint64_t x = ld64(S.in, m + l) ^ ld64(S.in, m - off + l);
+                                    if (x) { l += __builtin_ctzll(x) >> 3; exact = true; break; }
+                                    l += 8;
+                                }
+                                if (l >= lim) { l = lim; exact = true; }
                                 if (exact) {
-                                    S.info[m - R0] = off | (len << 16);
-                                    rmask |= bit;
+                                    S.info[m - R0] = off | (l << 16);
+                                    len = l;
                                 } else if (trusted) {
                                     need = true;
                                     nm = m;
                                     noff = off;
-                                    nlen = len;
                                 } else {
                                     unknown = true;
                                     active = false;
                                 }
                             }
                             if (!need && !unknown) {
+                                if (first_m == 0xFFFFFFFFu) {
+                                    first_m = m;
+                                    rest += 3 + ext_bytes(len - 4);
+                                } else {
+                                    rest += seq_size(m - last_end, len);
+                                }
                                 p = m + len;
                                 last_end = p;
                                 active = p < seg_hi;
                             }
                         }
                     }
-                    // cooperative extension of long matches (whole wave, 256 B/step)
+                    // cooperative extension of long matches (whole wave, 512 B/step)
                     unsigned long long nmask = __ballot(need);
                     while (nmask) {
                         const int l = __ffsll((long long)nmask) - 1;
                         nmask &= nmask - 1;
-                        const uint32_t m = __shfl(nm, l, 64), off = __shfl(noff, l, 64);
+                        const uint32_t m = lane_val(nm, l), off = lane_val(noff, l);
                         const uint32_t lim = mlimit - m;
-                        uint32_t len = __shfl(nlen, l, 64);
+                        uint32_t len = kLaneExt;
                         for (;;) {
-                            const uint32_t k = len + 4u * lane;
-                            uint32_t x = 0;
+                            const uint32_t k = len + 8u * lane;
+                            uint64_t x = 0;
                             const bool in_range = k < lim;
-                            if (in_range) x = ld32(S.in, m + k) ^ ld32(S.in, m - off + k);
+                            if (in_range) x = ld64(S.in, m + k) ^ ld64(S.in, m - off + k);
                             const unsigned long long bad = __ballot(in_range && x != 0);
                             if (bad) {
                                 const int fl = __ffsll((long long)bad) - 1;
-                                const uint32_t xf = __shfl(x, fl, 64);
-                                len = len + 4u * fl + (__builtin_ctz(xf) >> 3);
+                                const uint32_t xlo = lane_val((uint32_t)x, fl);
+                                const uint32_t xhi = lane_val((uint32_t)(x >> 32), fl);
+                                const uint64_t xf = ((uint64_t)xhi << 32) | xlo;
+                                len = len + 8u * fl + (__builtin_ctzll(xf) >> 3);
                                 break;
                             }
-                            len += 256;
+                            len += 512;
                             if (len >= lim) break;
                         }
                         if (len > lim) len = lim;
                         if (lane == l) {
                             S.info[m - R0] = off | (len << 16);
-                            rmask |= 1u << (m - seg_lo);
+                            if (first_m == 0xFFFFFFFFu) {
+                                first_m = m;
+                                rest += 3 + ext_bytes(len - 4);
+                            } else {
+                                rest += seq_size(m - last_end, len);
+                            }
                             p = m + len;
                             last_end = p;
                             active = p < seg_hi;
@@ -327,15 +374,7 @@ lz4_encode_kernel(BlockArgs a) {
                     }
                 }
                 ex = (entry < seg_hi) ? p : entry;
-                const uint32_t kv = unknown ? 0u : ex;
-                uint32_t mx = kv;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    uint32_t y = __shfl_up(mx, d, 64);
-                    if (lane >= d) mx = mx > y ? mx : y;
-                }
-                uint32_t prev = __shfl_up(mx, 1, 64);
-                if (lane == 0) prev = 0;
+                const uint32_t prev = wave_shr1(wave_incl_max(unknown ? 0u : ex), 0u);
                 const uint32_t ne = prev > floor_e ? prev : floor_e;
                 const bool bad = (ne != entry) || unknown;
                 entry = ne;
@@ -345,77 +384,62 @@ lz4_encode_kernel(BlockArgs a) {
             }
             STAT(4);
             STAT_ADD(9, it_done);
-            // anchors: inclusive max-scan of last match ends
-            uint32_t incl = last_end;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                uint32_t y = __shfl_up(incl, d, 64);
-                if (lane >= d) incl = incl > y ? incl : y;
+            // anchors: max of earlier walkers' last match ends (and the carried one)
+            const uint32_t carry_a = S.carry_a;
+            const uint32_t incl = wave_incl_max(last_end);
+            const uint32_t excl = wave_shr1(incl, 0u);
+            const uint32_t anchor_in = excl > carry_a ? excl : carry_a;
+            uint32_t bytes = rest;
+            if (first_m != 0xFFFFFFFFu) {
+                const uint32_t lit = first_m - anchor_in;
+                bytes += ext_bytes(lit) + lit;
             }
-            uint32_t excl = __shfl_up(incl, 1, 64);
-            const uint32_t anchor_in = (lane == 0) ? S.carry_a : (excl > S.carry_a ? excl : S.carry_a);
-            // sizes
-            uint32_t bytes = 0;
-            {
-                uint32_t p = entry, an = anchor_in;
-                while (p < seg_hi) {
-                    const uint32_t w = mword & (0xFFFFFFFFu << (p - seg_lo));
-                    if (!w) break;
-                    const uint32_t m = seg_lo + __builtin_ctz(w);
-                    const uint32_t len = S.info[m - R0] >> 16;
-                    bytes += seq_size(m - an, len);
-                    p = an = m + len;
-                }
-            }
+            const uint32_t o0 = S.cursor + wave_excl_scan(bytes);
+            const uint32_t total = lane_val(o0 + bytes, 63);
+            S.seg_entry[lane] = entry;
+            S.seg_anchor[lane] = anchor_in;
+            S.seg_out[lane] = o0;
             STAT(5);
-            const uint32_t base = S.cursor;
-            const uint32_t o0 = base + wave_excl_scan(bytes);
-            const uint32_t total = __shfl(o0 + bytes, 63, 64);
-            const bool ovf = total + 16 > (uint32_t)kOutCap;  // keep room for the last token
-            S.dl_len[lane] = 0;
-            if (!ovf) {
-                uint32_t p = entry, an = anchor_in, o = o0;
-                while (p < seg_hi) {
-                    const uint32_t w = mword & (0xFFFFFFFFu << (p - seg_lo));
-                    if (!w) break;
-                    const uint32_t m = seg_lo + __builtin_ctz(w);
-                    const uint32_t v = S.info[m - R0];
-                    const uint32_t len = v >> 16, off = v & 0xFFFFu;
-                    const uint32_t lit = m - an, ml = len - 4;
-                    out[o++] = (uint8_t)(((lit < 15 ? lit : 15) << 4) | (ml < 15 ? ml : 15));
-                    o += put_len(out + o, lit);
-                    if (lit <= (uint32_t)kLongLit) {
-                        for (uint32_t k = 0; k < lit; k++) out[o + k] = S.in[an + k];
-                    } else {
-                        S.dl_src[lane] = an;
-                        S.dl_dst[lane] = o;
-                        S.dl_len[lane] = lit;
-                    }
-                    o += lit;
-                    out[o] = (uint8_t)off;
-                    out[o + 1] = (uint8_t)(off >> 8);
-                    o += 2;
-                    o += put_len(out + o, ml);
-                    p = an = m + len;
-                }
-            }
-            STAT(6);
-            // deferred long literal runs, cooperatively
-            unsigned long long lm = __ballot(!ovf && S.dl_len[lane] != 0);
-            while (lm) {
-                const int l = __ffsll((long long)lm) - 1;
-                lm &= lm - 1;
-                const uint32_t s0 = S.dl_src[l], d0 = S.dl_dst[l], ln = S.dl_len[l];
-                for (uint32_t k = lane; k < ln; k += 64) out[d0 + k] = S.in[s0 + k];
-            }
             if (lane == 63) {
                 S.carry_p = ex;
-                const uint32_t la = incl > S.carry_a ? incl : S.carry_a;
-                S.carry_a = la;
+                S.carry_a = incl > carry_a ? incl : carry_a;
                 S.cursor = total;
-                if (ovf) S.overflow = 1;
+                if (total + 16 > (uint32_t)kOutCap) S.overflow = 1;  // keep room for the tail
             }
         }
+        __syncthreads();
+        // ---- E: emission by all 8 waves: 8 threads per walker segment; thread k
+        // writes the k-th sequence (a segment holds <= 8), the 8 share long literals
+        if (parse_round && !S.overflow) {
+            const int l = tid >> 3, k = tid & 7;
+            const uint32_t seg_lo = R0 + l * kSegE, seg_hi = seg_lo + kSegE;
+            const uint32_t mword = S.mask[l];
+            uint32_t p = S.seg_entry[l], an = S.seg_anchor[l], o = S.seg_out[l];
+            for (int i = 0; p < seg_hi; i++) {
+                const uint32_t w = mword & (0xFFFFFFFFu << (p - seg_lo));
+                if (!w) break;
+                const uint32_t m = seg_lo + __builtin_ctz(w);
+                const uint32_t v = S.info[m - R0];
+                const uint32_t len = v >> 16, off = v & 0xFFFFu;
+                const uint32_t lit = m - an, ml = len - 4;
+                const uint32_t hdr = 1 + ext_bytes(lit);
+                if (i == k) {
+                    out[o] = (uint8_t)(((lit < 15 ? lit : 15) << 4) | (ml < 15 ? ml : 15));
+                    put_len(out + o + 1, lit);
+                    uint8_t *q = out + o + hdr + lit;
+                    q[0] = (uint8_t)off;
+                    q[1] = (uint8_t)(off >> 8);
+                    put_len(q + 2, ml);
+                    if (lit <= (uint32_t)kLongLit)
+                        for (uint32_t t = 0; t < lit; t++) out[o + hdr + t] = S.in[an + t];
+                }
+                if (lit > (uint32_t)kLongLit)  // all 8 threads of the segment
+                    for (uint32_t t = k; t < lit; t += 8) out[o + hdr + t] = S.in[an + t];
+                o += hdr + lit + 2 + ext_bytes(ml);
+                p = an = m + len;
+            }
+        }
+        STAT(6);
         __syncthreads();
         STAT(7);
         STAT_ADD(10, 1);

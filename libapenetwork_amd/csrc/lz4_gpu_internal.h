@@ -17,21 +17,51 @@ constexpr int kErange = -2147483647 - 1;
 // ---- wave64 helpers ----
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
-// Exclusive prefix sum over the 64 lanes of a wave.
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) {
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
-        if (lane_id() >= d) x += y;
-    }
-    return x - v;
+// DPP lane moves (GFX9-family controls, available on gfx950): lanes whose
+// source is outside the row / masked off keep `old`.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114,
+              kDppRowShr8 = 0x118, kDppBcast15 = 0x142, kDppBcast31 = 0x143,
+              kDppWaveShr1 = 0x138;
+
+// Inclusive scans over the 64 lanes (Hillis-Steele inside 16-lane rows, then
+// row broadcasts) -- VALU latency instead of LDS-crossbar shuffles.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    x += dpp<kDppRowShr1>(0u, x);
+    x += dpp<kDppRowShr2>(0u, x);
+    x += dpp<kDppRowShr4>(0u, x);
+    x += dpp<kDppRowShr8>(0u, x);
+    x += dpp<kDppBcast15, 0xA>(0u, x);
+    x += dpp<kDppBcast31, 0xC>(0u, x);
+    return x;
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = umax(x, dpp<kDppRowShr1>(0u, x));
+    x = umax(x, dpp<kDppRowShr2>(0u, x));
+    x = umax(x, dpp<kDppRowShr4>(0u, x));
+    x = umax(x, dpp<kDppRowShr8>(0u, x));
+    x = umax(x, dpp<kDppBcast15, 0xA>(0u, x));
+    x = umax(x, dpp<kDppBcast31, 0xC>(0u, x));
+    return x;
+}
+
+// value of the previous lane (lane 0 gets `first`)
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x, uint32_t first) {
+    return dpp<kDppWaveShr1>(first, x);
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) {
+    return wave_shr1(wave_incl_sum(v), 0u);
+}
+
+__device__ __forceinline__ uint32_t lane_val(uint32_t v, int l) {  // l wave-uniform
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
 
 // ---- diagnostic phase timers (built only into libape_lz4_amd_stats.so) ----
