@@ -23,9 +23,9 @@
  * Return value of a launcher: 0 on success, otherwise a negative
  * APE_LZ4_GPU_E* code (nothing was launched); per-block status is in d_result.
  *
- * GPU limits: blocks are at most APE_LZ4_GPU_MAX_BLOCK (65536) bytes on the
- * uncompressed side (the LZ4 window; the benchmark's 64 KiB block).  A block
- * whose decoded output would exceed it gets d_result = APE_LZ4_GPU_ERANGE.
+ * GPU limits: the encoder takes blocks of at most APE_LZ4_GPU_MAX_BLOCK (65536)
+ * bytes (the LZ4 window; the benchmark's 64 KiB block); a larger input gets
+ * d_result = APE_LZ4_GPU_ERANGE.  The decoder has no block-size limit.
  */
 #pragma once
 #include <stddef.h>

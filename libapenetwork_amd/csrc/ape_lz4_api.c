@@ -55,11 +55,6 @@ static int gpu_decompress(const char *src, char *dst, int csize, int cap, int pa
 {
     int rt = 0, r = ape_lz4_gpu_decompress_one(src, dst, csize, cap, partial, target, &rt);
     if (rt) { gpu_failed(rt); return -1; }
-    if (r == APE_LZ4_GPU_ERANGE) {
-        fprintf(stderr, "libape_lz4_amd: decoded block exceeds the GPU block limit (%d)\n",
-                APE_LZ4_GPU_MAX_BLOCK);
-        return -1;
-    }
     return r;
 }
 

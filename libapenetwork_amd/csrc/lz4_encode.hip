@@ -47,9 +47,11 @@ constexpr uint32_t kLaneExt = 256;      // lane-serial match measuring budget (b
 constexpr uint32_t kEager = 36;         // phase C measures matches up to this length
 constexpr uint32_t kTrunc = 0xFFFFu;    // info length field: "at least kEager"
 
+// `in` first: its dword reads (ld32/ld64) must be 4-byte aligned in LDS, or
+// every one of them takes the unaligned-access stall.
 struct __attribute__((aligned(16))) EncShared {
-    uint8_t out[kOutCap + 32];
     uint8_t in[kMaxBlock + 64];
+    uint8_t out[(kOutCap + 32 + 15) & ~15];
     uint32_t E[kHashSize];
     uint32_t info[kRound];
     uint32_t mask[kRound / kSegE];
@@ -57,6 +59,9 @@ struct __attribute__((aligned(16))) EncShared {
     uint32_t carry_p, carry_a, cursor;
     int overflow;
 };
+static_assert(offsetof(EncShared, in) % 16 == 0 && offsetof(EncShared, out) % 16 == 0 &&
+                  offsetof(EncShared, E) % 16 == 0,
+              "LDS arrays read by dwords / written by 16-byte stores must be aligned");
 
 // bytes [sh, sh+4) of the little-endian 8-byte word hi:lo
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {

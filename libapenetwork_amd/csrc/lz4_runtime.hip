@@ -138,8 +138,7 @@ int host_batch(int mode, const char *const *h_src, const int *h_in, char *const 
             size_t bound = (size_t)n + n / 255 + 16;
             lim = h_cap[i] <= 0 ? 0 : ((size_t)h_cap[i] < bound ? (size_t)h_cap[i] : bound);
         } else {
-            lim = h_cap[i] <= 0 ? 0 : ((size_t)h_cap[i] < (size_t)kMaxBlock ? (size_t)h_cap[i]
-                                                                         : (size_t)kMaxBlock);
+            lim = h_cap[i] <= 0 ? 0 : (size_t)h_cap[i];  // the decoder has no block limit
         }
         out_len[i] = lim;
         pos += up16(lim ? lim : 1);

@@ -109,14 +109,18 @@ def test_misaligned_buffers(cuda, product, oracle):
     assert outs == srcs
 
 
-def test_gpu_block_limit(cuda, product, oracle):
-    big = I.make("text", 70000)
-    _, c = orc_compress(oracle, big)
-    small = I.make("comp", 40000)
-    _, c2 = orc_compress(oracle, small)
-    rs, outs = run_decode(cuda, product, [c, c2], [70000, 70000])
-    assert rs[0] == product.ERANGE
-    assert rs[1] == 40000 and outs[1] == small
+def test_blocks_beyond_64k(cuda, product, oracle):
+    """The decoder has no block-size limit (only the 64 KiB offset window)."""
+    srcs = [I.make("text", 70000), I.make("comp", 40000), I.make("rand", 200000, seed=3),
+            I.make("zeros", 300000), I.make("period7", 131072), I.make("comp", 1 << 20, seed=9)]
+    comps = [orc_compress(oracle, s)[1] for s in srcs]
+    caps = [len(s) for s in srcs]
+    rs, outs = run_decode(cuda, product, comps, caps)
+    assert rs == caps
+    assert outs == srcs
+    # and an undersized cap fails exactly like the reference
+    rs, _ = run_decode(cuda, product, comps, [c - 1 for c in caps])
+    assert rs == [orc_decompress(oracle, c, n - 1)[0] for c, n in zip(comps, caps)]
 
 
 def test_strided_batch_benchmark_layout(cuda, product, oracle):

@@ -13,8 +13,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["APE_LZ4_LIB"] = os.path.join(ROOT, "libapenetwork_amd", "libape_lz4_amd_stats.so")
 sys.path.insert(0, ROOT)
 
-DEC = ["init", "stage", "walk-fixpoint", "count+scan", "validate", "-", "barrier-after-walk",
-       "copy", "(chunks)", "flush", "(blocks)", "", "", "", "", ""]
+DEC = ["parse", "copy", "(batches)", "(steps)", "(restages)", "", "", "", "", "", "(blocks)", "", "", "",
+       "", ""]
 ENC = ["load+init", "A hash+min", "B read", "C roll+verify", "D fixpoint", "D sizes", "E emit",
        "E deferred+barrier", "last+flush", "(fixpoint iters)", "(rounds)", "(blocks)", "", "", "",
        ""]
