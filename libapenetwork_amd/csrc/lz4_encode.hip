@@ -4,134 +4,178 @@
 // 811-815 -> LZ4_compress_generic :530-755, byU16 / noDict).  The output is a
 // valid LZ4 v1.7.1 block -- it obeys every parsing rule decompress_safe enforces
 // (:1346-1366, :1375, :1444-1447): matches start at <= n-12, end at <= n-5, the
-// last >= 5 bytes are literals -- but it is produced by a parallel parse, not
-// by the reference's sequential skip-search, so the bytes differ.
+// last >= 5 bytes are literals -- but it is produced by a round-parallel parse,
+// not by the reference's sequential search, so the bytes differ.
 //
-// One 512-thread workgroup per block, everything in LDS (~153 KiB, 1 block/CU):
-//   in[64 KiB]     the input block
-//   E[4096]        hash table, u32 = (latest position of earlier rounds) << 16
-//                  | (earliest position of the current round, 0xFFFF = none)
-//   info[2048]     per position of the current round: best match (offset |
-//                  length << 16), length 0xFFFF = "at least kEager, extend on use"
-//   out[~64.3 KiB] the compressed block, flushed to HBM with 16-byte stores.
-// The block is processed in rounds of kRound = 2048 positions:
-//   A. every position hashes its 5 bytes (the reference's 64-bit hash,
-//      :456-462) and atomicMin's itself into the low half of E[h];
-//   B. every position reads E[h]: candidate T (latest earlier-round position)
-//      and L (earliest same-round position, if before it);
-//   C. atomicMax rolls E[h] to (latest position of this round) | 0xFFFF; each
-//      position verifies both candidates and measures them up to kEager bytes
-//      with independent 8-byte LDS compares (all loads in flight at once);
-//   D. wave 0 runs the greedy parse: 64 walkers each own 32 positions, jump
-//      match-to-match through a per-segment "has match" bitmask, and iterate to
-//      the fixpoint where every walker's entry equals the chain position reaching
-//      it (identical to a sequential greedy parse from position 0); DPP scans
-//      give entries, anchors and output offsets;
-//   E. all 8 waves emit: 8 threads per walker segment, one sequence each.
-// Atomic min/max make the table state independent of thread timing, so the
-// output is a deterministic function of the input.
+// One wave (one 64-thread workgroup) per block.  A batch holds ~1M blocks, so
+// the parallelism comes from many blocks in flight; per wave the LDS holds only
+// the reference's own hash table (8192 x u16, 13-bit hash of 5 bytes, :449-462)
+// plus a 1 KiB scratch, ~17 KiB, so 9 blocks share a CU.  The input stays in
+// HBM/L2 and is read with unaligned 16-byte loads.
+//
+// The block is parsed in rounds of 64 positions starting at the parse position P:
+//  1. every lane p = P + lane loads in[p-4, p+28), hashes in[p, p+5) and reads
+//     two candidates: T = table[h] (positions walked in earlier rounds, as the
+//     reference inserts them: :595-619, :680-706) and L = the earliest lane of
+//     this round with the same low hash bits (found with an LDS atomicMin);
+//     it loads in[c-4, c+28) for both, verifies 4 bytes, measures the match up
+//     to 28 bytes and how far it extends backwards (up to 4 bytes);
+//  2. the scalar unit walks the greedy chain through the round: jump to the
+//     next lane with a match (ballot mask), extend it backwards into pending
+//     literals (the reference's catch-up, :628-629) and, for a match that
+//     reached 28 bytes, forwards with the whole wave (1 KiB per step);
+//  3. walked positions and match_end - 2 (:680) go into the table;
+//  4. member lanes emit their sequences straight to dst (prefix sums give the
+//     offsets), a literal run longer than 32 bytes is copied by the whole wave.
+// Last literals (:732-751) are copied by the whole wave with 16-byte moves.
+#include <string.h>
+
 #include "lz4_gpu_internal.h"
 
 namespace apelz4 {
 
 namespace {
 
-constexpr int kThreads = 512;
-constexpr int kRound = 2048;            // positions per round (4 per thread)
-constexpr int kHashLog = 12;
-constexpr int kHashSize = 1 << kHashLog;
-constexpr int kSegE = 32;               // positions per walker segment
-constexpr int kOutCap = kMaxBlock + kMaxBlock / 255 + 16;  // compressBound(64 KiB)
-constexpr int kLongLit = 64;
-constexpr uint32_t kLaneExt = 256;      // lane-serial match measuring budget (bytes)
-constexpr uint32_t kEager = 36;         // phase C measures matches up to this length
-constexpr uint32_t kTrunc = 0xFFFFu;    // info length field: "at least kEager"
+#ifndef APE_LZ4_HLOG
+#define APE_LZ4_HLOG 13
+#endif
+constexpr int kHLog = APE_LZ4_HLOG;
+constexpr int kHSize = 1 << kHLog;
+constexpr uint32_t kEagerLen = 28;   // match bytes measured before the walk
+constexpr uint32_t kLongLit = 32;    // longer literal runs are copied by the wave
+#ifndef APE_LZ4_ERING
+#define APE_LZ4_ERING 8192
+#endif
+constexpr uint32_t kRingE = APE_LZ4_ERING;  // per-wave ring of recent input bytes
+constexpr uint32_t kChunkE = 512;    // ring refill granule (8 bytes per lane)
+constexpr uint32_t kAhead = 1024;    // keep the ring filled this far past P
 
-// `in` first: its dword reads (ld32/ld64) must be 4-byte aligned in LDS, or
-// every one of them takes the unaligned-access stall.
-struct __attribute__((aligned(16))) EncShared {
-    uint8_t in[kMaxBlock + 64];
-    uint8_t out[(kOutCap + 32 + 15) & ~15];
-    uint32_t E[kHashSize];
-    uint32_t info[kRound];
-    uint32_t mask[kRound / kSegE];
-    uint32_t seg_entry[64], seg_anchor[64], seg_out[64];  // walker results for emission
-    uint32_t carry_p, carry_a, cursor;
-    int overflow;
+struct __attribute__((aligned(16))) EncLds {
+    uint16_t tab[kHSize];
+    uint32_t scr[256];
+    uint32_t ring[kRingE / 4];       // input byte x at ring byte (x mod kRingE)
 };
-static_assert(offsetof(EncShared, in) % 16 == 0 && offsetof(EncShared, out) % 16 == 0 &&
-                  offsetof(EncShared, E) % 16 == 0,
-              "LDS arrays read by dwords / written by 16-byte stores must be aligned");
 
-// bytes [sh, sh+4) of the little-endian 8-byte word hi:lo
-__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
+// Compiler barrier for lane-to-lane communication through LDS inside one wave.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ uint32_t ld32(const uint8_t *in, uint32_t pos) {
-    const uint32_t *w = (const uint32_t *)(in + (pos & ~3u));
-    return funnel(w[1], w[0], pos & 3u);
-}
-
-// 8 bytes at pos (three aligned LDS dwords)
-__device__ __forceinline__ uint64_t ld64(const uint8_t *in, uint32_t pos) {
-    const uint32_t *w = (const uint32_t *)(in + (pos & ~3u));
-    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = pos & 3u;
-    return (uint64_t)funnel(w1, w0, sh) | ((uint64_t)funnel(w2, w1, sh) << 32);
-}
-
-// Common-prefix length (from byte 4 on) of positions p and c, up to kEager;
-// the four 8-byte compares are independent loads, so they are all in flight.
-__device__ __forceinline__ uint32_t eager_len(const uint8_t *in, uint32_t p, uint32_t c) {
-    uint64_t x[4];
+// 32 bytes in[pos, pos+32) as 8 dwords; bytes outside [0, n) read as 0.
+__device__ __forceinline__ void ld32b(const uint8_t *in, int n, int pos, uint32_t (&X)[8]) {
+    if (pos >= 0 && pos + 32 <= n) {
+        uint4 a, b;
+        __builtin_memcpy(&a, in + pos, 16);
+        __builtin_memcpy(&b, in + pos + 16, 16);
+        X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w;
+        X[4] = b.x; X[5] = b.y; X[6] = b.z; X[7] = b.w;
+    } else {
 #pragma unroll
-    for (int s = 0; s < 4; s++) x[s] = ld64(in, p + 4 + 8 * s) ^ ld64(in, c + 4 + 8 * s);
-    uint32_t len = kEager;
+        for (int k = 0; k < 8; k++) X[k] = 0;
+        for (int k = 0; k < 32; k++) {
+            const int q = pos + k;
+            if (q >= 0 && q < n) X[k >> 2] |= (uint32_t)in[q] << (8 * (k & 3));
+        }
+    }
+}
+
+// 8 input bytes at a (zero beyond n): one ring refill lane
+__device__ __forceinline__ uint2 chunk_load(const uint8_t *in, uint32_t n, uint32_t a) {
+    uint2 v = make_uint2(0u, 0u);
+    if (a + 8u <= n) {
+        __builtin_memcpy(&v, in + a, 8);
+    } else {
+        for (uint32_t t = 0; t < 8u && a + t < n; t++) {
+            const uint32_t by = (uint32_t)in[a + t] << (8 * (t & 3));
+            if (t < 4) v.x |= by; else v.y |= by;
+        }
+    }
+    return v;
+}
+
+__device__ __forceinline__ void chunk_store(EncLds &S, uint32_t f, int lane, uint2 v) {
+    *(uint2 *)&S.ring[((f + 8u * (uint32_t)lane) & (kRingE - 1)) >> 2] = v;
+}
+
+// Fill the ring with [f0, f0 + 2*kChunkE) now (after a jump past the filled bytes).
+__device__ __forceinline__ void ring_fill(EncLds &S, const uint8_t *in, uint32_t n, uint32_t f0,
+                                          int lane) {
+    const uint2 a = chunk_load(in, n, f0 + 8u * (uint32_t)lane);
+    const uint2 b = chunk_load(in, n, f0 + kChunkE + 8u * (uint32_t)lane);
+    chunk_store(S, f0, lane, a);
+    chunk_store(S, f0 + kChunkE, lane, b);
+}
+
+// 32 bytes at pos from the ring (pos >= fill - kRingE, or pos < 0 while the
+// ring's tail is still zero)
+__device__ __forceinline__ void ring32(const EncLds &S, int pos, uint32_t (&X)[8]) {
+    const uint32_t sh = (uint32_t)pos & 3u;
+    const int w0 = pos >> 2;
+    uint32_t W[9];
 #pragma unroll
-    for (int s = 3; s >= 0; s--)
-        if (x[s]) len = 4 + 8 * s + (__builtin_ctzll(x[s]) >> 3);
+    for (int k = 0; k < 9; k++) W[k] = S.ring[(uint32_t)(w0 + k) & (kRingE / 4 - 1)];
+#pragma unroll
+    for (int k = 0; k < 8; k++) X[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
+}
+
+// 4 input bytes at x from the ring
+__device__ __forceinline__ uint32_t ring4(const EncLds &S, uint32_t x) {
+    const uint32_t w = x >> 2;
+    return __builtin_amdgcn_alignbyte(S.ring[(w + 1) & (kRingE / 4 - 1)],
+                                      S.ring[w & (kRingE / 4 - 1)], x & 3u);
+}
+
+// the reference's hash of the 5 bytes at p (x1 = in[p..p+3], b4 = in[p+4])
+__device__ __forceinline__ uint32_t hash5(uint32_t x1, uint32_t b4) {
+    const uint64_t seq = (uint64_t)x1 | ((uint64_t)(b4 & 0xFFu) << 32);
+    return (uint32_t)((seq * 889523592379ULL) >> (40 - kHLog)) & (kHSize - 1);
+}
+
+// common length of X and Y from byte 4 (dword 1) on, up to kEagerLen
+__device__ __forceinline__ uint32_t eager(const uint32_t (&X)[8], const uint32_t (&Y)[8]) {
+    uint32_t len = kEagerLen;
+#pragma unroll
+    for (int k = 7; k >= 2; k--) {
+        const uint32_t d = X[k] ^ Y[k];
+        if (d) len = 4u * (uint32_t)(k - 1) + (__builtin_ctz(d) >> 3);
+    }
     return len;
 }
 
-__device__ __forceinline__ uint32_t hash5(uint32_t lo32, uint32_t b4) {
-    uint64_t seq = (uint64_t)lo32 | ((uint64_t)b4 << 32);
-    return (uint32_t)((seq * 889523592379ULL) >> (40 - kHashLog)) & (kHashSize - 1);
-}
-
-// Length of the match at m with offset off (first 4 bytes known equal), measured
-// up to min(lim, kLaneExt).  exact = false when the budget ran out first.
-__device__ __forceinline__ uint32_t measure(const uint8_t *in, uint32_t m, uint32_t off,
-                                            uint32_t lim, bool &exact) {
-    const uint32_t cap = lim < kLaneExt ? lim : kLaneExt;
-    uint32_t l = 4;
-    while (l < cap) {
-        const uint32_t x = ld32(in, m + l) ^ ld32(in, m - off + l);
-        if (x) {
-            l += __builtin_ctz(x) >> 3;
-            exact = true;
-            return l < lim ? l : lim;
-        }
-        l += 4;
-    }
-    exact = l >= lim;
-    return l < lim ? l : lim;
+// bytes equal just before the match (in[p-1] == in[c-1], ...), 0..4
+__device__ __forceinline__ uint32_t back4(uint32_t x0, uint32_t y0) {
+    const uint32_t d = x0 ^ y0;
+    return d ? (__builtin_clz(d) >> 3) : 4u;
 }
 
 __device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {  // bytes after a 15 nibble
     return v >= 15 ? (v - 15) / 255 + 1 : 0;
 }
 
-__device__ __forceinline__ uint32_t seq_size(uint32_t lit, uint32_t len) {
-    return 1 + ext_bytes(lit) + lit + 2 + ext_bytes(len - 4);
-}
-
-__device__ __forceinline__ uint32_t put_len(uint8_t *o, uint32_t v) {  // returns bytes written
+// write the length extension of v (>= 15) at o, returns bytes written
+__device__ __forceinline__ uint32_t put_len(uint8_t *o, uint32_t v) {
     if (v < 15) return 0;
     v -= 15;
     uint32_t k = 0;
     for (; v >= 255; v -= 255) o[k++] = 255;
     o[k++] = (uint8_t)v;
     return k;
+}
+
+// Copy in[a, a+len) to dst[o, o+len) with the whole wave (16 bytes per lane per step).
+__device__ __forceinline__ void wave_copy(const uint8_t *in, uint8_t *dst, uint32_t a, uint32_t o,
+                                          uint32_t len, int lane) {
+    for (uint32_t k = 16u * (uint32_t)lane; k < len; k += 1024u) {
+        if (k + 16u <= len) {
+            uint4 v;
+            __builtin_memcpy(&v, in + a + k, 16);
+            __builtin_memcpy(dst + o + k, &v, 16);
+        } else {
+            for (uint32_t t = k; t < len; t++) dst[o + t] = in[a + t];
+        }
+    }
 }
 
 }  // namespace
@@ -148,349 +192,295 @@ hipError_t enc_stats_read(unsigned long long *out, int reset) {
 }
 #endif
 
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(64)
 lz4_encode_kernel(BlockArgs a) {
-    __shared__ EncShared S;
+    __shared__ EncLds S;
     const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
+    const int lane = threadIdx.x;
 
-    const uint8_t *src =
+    const uint8_t *in =
         (const uint8_t *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
     uint8_t *dst = (uint8_t *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
     const int n = a.src_size[b];
-    const int cap = a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride;
+    const uint32_t cap = (uint32_t)(a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride);
     if (n < 0 || n > kMaxBlock) {
-        if (tid == 0) a.result[b] = n < 0 ? 0 : kErange;
+        if (lane == 0) a.result[b] = n < 0 ? 0 : kErange;
         return;
     }
-    uint8_t *out = S.out + ((uintptr_t)dst & 15);
+    if ((int)cap < 0) {
+        if (lane == 0) a.result[b] = 0;
+        return;
+    }
 
     STATS_DECL
-    // ---- load the block (16-byte loads when aligned) and init the table ----
-    if ((((uintptr_t)src) & 15) == 0) {
-        const int n16 = n & ~15;
-        for (int k = 16 * tid; k < n16; k += 16 * kThreads)
-            *(uint4 *)(S.in + k) = *(const uint4 *)(src + k);
-        for (int k = n16 + tid; k < n; k += kThreads) S.in[k] = src[k];
-    } else {
-        for (int k = tid; k < n; k += kThreads) S.in[k] = src[k];
-    }
-    if (tid < 64) S.in[n + tid] = 0;
-    for (int i = tid; i < kHashSize; i += kThreads) S.E[i] = 0x0000FFFFu;
-    if (tid == 0) {
-        S.carry_p = 0;
-        S.carry_a = 0;
-        S.cursor = 0;
-        S.overflow = 0;
-    }
-    __syncthreads();
-    STAT(0);
+    // table = 0 (the reference's memset state: position 0 for every hash)
+    for (int i = lane; i < kHSize / 8; i += 64) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
+    for (int i = lane; i < 256; i += 64) S.scr[i] = 0xFFFFFFFFu;
+    for (int i = lane; i < (int)(kRingE / 16); i += 64) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
+    wave_sync();
+    uint32_t fill = 2 * kChunkE;  // ring holds input [rlo, fill)
+    uint32_t rlo = 0;
+    ring_fill(S, in, (uint32_t)n, 0u, lane);
+    wave_sync();
 
-    const uint32_t hash_end = n >= 5 ? (uint32_t)(n - 5) : 0;  // hash positions p <= n-5
-    const bool any_hash = n >= 5;
-    const uint32_t mstart_end = n >= 12 ? (uint32_t)(n - 12) : 0;  // match starts p <= n-12
-    const uint32_t mlimit = n >= 5 ? (uint32_t)(n - 5) : 0;        // match ends <= n-5
+    uint32_t anchor = 0;     // start of the pending literals (wave-uniform)
+    uint32_t o = 0;          // output cursor
+    bool overflow = false;
+    const uint32_t un = (uint32_t)n;
+    const uint32_t mstart = un >= 12 ? un - 12 : 0;   // matches start at <= n-12 (:585)
+    const uint32_t mlimit = un >= 5 ? un - 5 : 0;     // and end at <= n-5 (:633)
+    uint32_t P = 0;
+    if (n < kMinLength) P = un;                       // :584 -> last literals only
 
-    for (uint32_t R0 = 0; R0 < (uint32_t)n; R0 += kRound) {
-        // ---- A: hash own 4 positions, atomicMin into the low half ----
-        const uint32_t p0 = R0 + 4 * tid;
-        uint32_t h[4], lo32[4];
-        {
-            const uint32_t *w = (const uint32_t *)(S.in + p0);
-            uint32_t w0 = w[0], w1 = w[1];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                lo32[j] = funnel(w1, w0, (uint32_t)j);
-                uint32_t b4 = (w1 >> (8 * j)) & 0xFFu;
-                h[j] = hash5(lo32[j], b4);
-            }
+    while (P < un && !overflow) {
+        // ---- 0. input ring: refill after a jump, prefetch the next chunk ----
+        if (fill < P + 96u) {
+            fill = (P >= 64u ? P - 64u : 0u) & ~7u;
+            rlo = fill;
+            wave_sync();
+            ring_fill(S, in, un, fill, lane);
+            fill += 2 * kChunkE;
+            wave_sync();
         }
-        if (tid < kRound / kSegE) S.mask[tid] = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            uint32_t p = p0 + j;
-            if (any_hash && p <= hash_end) {
-                uint32_t e = S.E[h[j]];
-                atomicMin(&S.E[h[j]], (e & 0xFFFF0000u) | p);
-            }
-        }
-        __syncthreads();
-        STAT(1);
-        // ---- B: read candidates ----
-        uint32_t cT[4], cL[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            uint32_t e = S.E[h[j]];
-            cT[j] = e >> 16;
-            cL[j] = e & 0xFFFFu;
-        }
-        __syncthreads();
-        STAT(2);
-        // ---- C: roll the table, verify candidates ----
-        // (positions before the carried chain position can never start a sequence)
-        const uint32_t carry_now = S.carry_p;
-        uint32_t nib = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            uint32_t p = p0 + j;
-            if (any_hash && p <= hash_end) atomicMax(&S.E[h[j]], (p << 16) | 0xFFFFu);
-            uint32_t best = 0;
-            if (p >= 1 && p <= mstart_end && n >= 13 && p >= carry_now) {
-                const bool okT = cT[j] < p && ld32(S.in, cT[j]) == lo32[j];
-                const bool okL = cL[j] < p && cL[j] != cT[j] && ld32(S.in, cL[j]) == lo32[j];
-                const uint32_t lim = mlimit - p;
-                // measure both (independent loads), keep the longer, then the closer
-                uint32_t lT = okT ? eager_len(S.in, p, cT[j]) : 0u;
-                uint32_t lL = okL ? eager_len(S.in, p, cL[j]) : 0u;
-                if (lT > lim) lT = lim;
-                if (lL > lim) lL = lim;
-                const bool pickL = okL && (!okT || lL > lT || (lL == lT && cL[j] > cT[j]));
-                const uint32_t len = pickL ? lL : lT;
-                if (okT || okL) {
-                    const uint32_t off = p - (pickL ? cL[j] : cT[j]);
-                    // a match that reached kEager before the limit may be longer
-                    best = off | ((len >= kEager && len < lim ? kTrunc : len) << 16);
-                    nib |= 1u << j;
-                }
-            }
-            S.info[p - R0] = best;
-        }
-        if (nib) atomicOr(&S.mask[(4 * tid) / kSegE], nib << ((4 * tid) % kSegE));
-        __syncthreads();
-        STAT(3);
+        const bool refill = fill < P + kAhead;
+        uint2 pre = make_uint2(0u, 0u);
+        if (refill) pre = chunk_load(in, un, fill + 8u * (uint32_t)lane);
 
-        // ---- D/E: greedy parse and emission (wave 0); skipped when the carried
-        // match covers the whole round ----
-        const bool parse_round = carry_now < R0 + kRound;
-        if (wave == 0 && parse_round) {
-            const uint32_t seg_lo = R0 + lane * kSegE;
-            const uint32_t seg_hi = seg_lo + kSegE;
-            const uint32_t carry = carry_now;
-            const uint32_t mword = S.mask[lane];
-            // Entries are lower-bounded by max(seg_lo, carry) and, on the true chain,
-            // equal the max of all earlier walkers' exits (chain positions only grow).
-            const uint32_t floor_e = seg_lo > carry ? seg_lo : carry;
-            uint32_t entry = floor_e;
-            uint32_t ex = 0, last_end = 0;  // last_end: end of my last match, 0 = none
-            uint32_t first_m = 0, rest = 0; // first match start; bytes of my sequences
-                                            // except the first one's literal run
-            int conf = 1;                   // walkers [0, conf) have exact entries
-            int it_done = 0;
-            (void)it_done;
-            for (int it = 0; it < 4 * 64; it++) {
-                it_done = it + 1;
-                // Only walkers with an exact entry may pay for extending a long match;
-                // a guessing walker that meets one stops with an unknown exit.
-                const bool trusted = lane < conf;
-                uint32_t p = entry;
-                last_end = 0;
-                first_m = 0xFFFFFFFFu;
-                rest = 0;
-                bool active = p < seg_hi, need = false, unknown = false;
-                uint32_t nm = 0, noff = 0;
-                while (__any(active)) {
-                    if (active && !need) {
-                        const uint32_t w = mword & (0xFFFFFFFFu << (p - seg_lo));
-                        if (!w) {
-                            p = seg_hi;
-                            active = false;
+        // ---- 1. candidates for p = P + lane ----
+        const uint32_t p = P + (uint32_t)lane;
+        uint32_t X[8];
+        ring32(S, (int)p - 4, X);
+        const bool hashable = p + 5 <= un;
+        const uint32_t h = hash5(X[1], X[2]);
+        const uint32_t cT = S.tab[h];
+        const uint32_t hs = h & 255u;
+        if (hashable) atomicMin(&S.scr[hs], (uint32_t)lane);
+        wave_sync();
+        const uint32_t jL = hashable ? S.scr[hs] : 0xFFFFFFFFu;
+        wave_sync();
+        if (hashable) S.scr[hs] = 0xFFFFFFFFu;
+        const bool can = p >= 1u && p <= mstart && n >= kMinLength;
+        const uint32_t cL = P + jL;
+        const bool tryT = can && cT < p;
+        const bool tryL = can && jL < (uint32_t)lane && cL != cT;
+        uint32_t Y[8], Z[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) { Y[k] = 0; Z[k] = 0; }
+        if (tryT) {
+            // recent candidates come from the ring, older ones from HBM / L2
+            if (cT >= rlo + 4u) ring32(S, (int)cT - 4, Y);
+            else ld32b(in, n, (int)cT - 4, Y);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) Z[k] = (uint32_t)__shfl((int)X[k], (int)(jL & 63u), 64);
+        if (!tryL) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) Z[k] = 0;
+        }
+        const bool okT = tryT && Y[1] == X[1];
+        const bool okL = tryL && Z[1] == X[1];
+        const uint32_t lim = can ? mlimit - p : 0u;  // longest match allowed here
+        uint32_t lT = okT ? eager(X, Y) : 0u, lL = okL ? eager(X, Z) : 0u;
+        // a length that reached kEagerLen is "at least"; compare as such
+        const bool pickL = okL && (!okT || lL > lT || (lL == lT && cL > cT));
+        const uint32_t c = pickL ? cL : cT;
+        uint32_t len = pickL ? lL : lT;
+        const bool trunc = len >= kEagerLen && lim > kEagerLen;
+        if (len > lim) len = lim;
+        const uint32_t bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), c);  // c - back >= 0
+        const bool has = okT || okL;
+        // lane info: len (16) | back (3) << 16 | trunc << 19
+        const uint32_t info = len | (bk << 16) | (trunc ? (1u << 19) : 0u);
+        const uint64_t Mm = __ballot(has);
+        STAT(0);
+
+        // ---- 2. greedy walk (scalar) ----
+        const uint32_t anchor0 = anchor;
+        uint32_t q = P;                 // walk position
+        uint64_t walked = 0, members = 0;
+        uint32_t m_back = 0, m_len = 0; // per member lane
+        for (;;) {
+            const uint32_t rel = q - P;
+            if (rel >= 64u) break;
+            const uint64_t w = Mm >> rel;
+            if (w == 0) {
+                walked |= ~0ull << rel;
+                q = P + 64u;
+                break;
+            }
+            const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
+            walked |= (~0ull << rel) & (j == 63 ? ~0ull : ((2ull << j) - 1ull));
+            const uint32_t v = lane_val(info, (int)j);
+            const uint32_t m = P + j;
+            uint32_t L = v & 0xFFFFu;
+            if (v & (1u << 19)) {
+                // forward extension with the whole wave, 1 KiB per step
+                const uint32_t cm = lane_val(c, (int)j);
+                const uint32_t lm = mlimit - m;
+                for (;;) {
+                    const uint32_t k = L + 16u * (uint32_t)lane;
+                    uint32_t d = 0;
+                    uint32_t at = 0;
+                    if (k < lm) {
+                        uint4 x, y;
+                        if (m + k + 16u <= un) {
+                            __builtin_memcpy(&x, in + m + k, 16);
+                            __builtin_memcpy(&y, in + cm + k, 16);
                         } else {
-                            const uint32_t m = seg_lo + __builtin_ctz(w);
-                            const uint32_t v = S.info[m - R0];
-                            uint32_t len = v >> 16;
-                            if (len == kTrunc) {
-                                // lane-serial extension within a budget; only a
-                                // longer match needs the cooperative path
-                                const uint32_t off = v & 0xFFFFu, lim = mlimit - m;
-                                uint32_t l = kEager;
-                                bool exact = false;
-                                while (l < lim && l < kLaneExt) {
-                                    const uint64_t x = ld64(S.in, m + l) ^ ld64(S.in, m - off + l);
-                                    if (x) { l += __builtin_ctzll(x) >> 3; exact = true; break; }
-                                    l += 8;
-                                }
-                                if (l >= lim) { l = lim; exact = true; }
-                                if (exact) {
-                                    S.info[m - R0] = off | (l << 16);
-                                    len = l;
-                                } else if (trusted) {
-                                    need = true;
-                                    nm = m;
-                                    noff = off;
-                                } else {
-                                    unknown = true;
-                                    active = false;
-                                }
+                            uint32_t xb[4] = {0, 0, 0, 0}, yb[4] = {0, 0, 0, 0};
+                            for (uint32_t t = 0; t < 16u && m + k + t < un; t++) {
+                                xb[t >> 2] |= (uint32_t)in[m + k + t] << (8 * (t & 3));
+                                yb[t >> 2] |= (uint32_t)in[cm + k + t] << (8 * (t & 3));
                             }
-                            if (!need && !unknown) {
-                                if (first_m == 0xFFFFFFFFu) {
-                                    first_m = m;
-                                    rest += 3 + ext_bytes(len - 4);
-                                } else {
-                                    rest += seq_size(m - last_end, len);
-                                }
-                                p = m + len;
-                                last_end = p;
-                                active = p < seg_hi;
-                            }
+                            x = make_uint4(xb[0], xb[1], xb[2], xb[3]);
+                            y = make_uint4(yb[0], yb[1], yb[2], yb[3]);
                         }
+                        const uint32_t e0 = x.x ^ y.x, e1 = x.y ^ y.y, e2 = x.z ^ y.z, e3 = x.w ^ y.w;
+                        if (e0) { d = 1; at = __builtin_ctz(e0) >> 3; }
+                        else if (e1) { d = 1; at = 4 + (__builtin_ctz(e1) >> 3); }
+                        else if (e2) { d = 1; at = 8 + (__builtin_ctz(e2) >> 3); }
+                        else if (e3) { d = 1; at = 12 + (__builtin_ctz(e3) >> 3); }
                     }
-                    // cooperative extension of long matches (whole wave, 512 B/step)
-                    unsigned long long nmask = __ballot(need);
-                    while (nmask) {
-                        const int l = __ffsll((long long)nmask) - 1;
-                        nmask &= nmask - 1;
-                        const uint32_t m = lane_val(nm, l), off = lane_val(noff, l);
-                        const uint32_t lim = mlimit - m;
-                        uint32_t len = kLaneExt;
-                        for (;;) {
-                            const uint32_t k = len + 8u * lane;
-                            uint64_t x = 0;
-                            const bool in_range = k < lim;
-                            if (in_range) x = ld64(S.in, m + k) ^ ld64(S.in, m - off + k);
-                            const unsigned long long bad = __ballot(in_range && x != 0);
-                            if (bad) {
-                                const int fl = __ffsll((long long)bad) - 1;
-                                const uint32_t xlo = lane_val((uint32_t)x, fl);
-                                const uint32_t xhi = lane_val((uint32_t)(x >> 32), fl);
-                                const uint64_t xf = ((uint64_t)xhi << 32) | xlo;
-                                len = len + 8u * fl + (__builtin_ctzll(xf) >> 3);
-                                break;
-                            }
-                            len += 512;
-                            if (len >= lim) break;
-                        }
-                        if (len > lim) len = lim;
-                        if (lane == l) {
-                            S.info[m - R0] = off | (len << 16);
-                            if (first_m == 0xFFFFFFFFu) {
-                                first_m = m;
-                                rest += 3 + ext_bytes(len - 4);
-                            } else {
-                                rest += seq_size(m - last_end, len);
-                            }
-                            p = m + len;
-                            last_end = p;
-                            active = p < seg_hi;
-                            need = false;
-                        }
+                    const uint64_t bad = __ballot(d != 0 || k >= lm);
+                    if (bad) {
+                        const int fl = __builtin_ctzll(bad);
+                        const uint32_t kk = L + 16u * (uint32_t)fl;
+                        L = kk >= lm ? lm : kk + lane_val(at, fl);
+                        break;
+                    }
+                    L += 1024u;
+                }
+                if (L > lm) L = lm;
+                STAT_ADD(12, 1);
+            }
+            uint32_t bkj = (v >> 16) & 7u;
+            if (bkj > m - anchor) bkj = m - anchor;   // never back into emitted bytes
+            if (lane == (int)j) { m_back = bkj; m_len = L + bkj; }
+            members |= 1ull << j;
+            q = m + L;
+            anchor = q;
+        }
+        STAT(1);
+
+        // ---- 3. table updates: walked positions, then match_end - 2 ----
+        if (((walked >> lane) & 1ull) && hashable) S.tab[h] = (uint16_t)p;
+        const bool mem = (members >> lane) & 1ull;
+        if (mem) {
+            const uint32_t e2 = p + (m_len - m_back) - 2u;   // match end - 2
+            if (e2 + 5u <= un) {
+                uint32_t lo32 = 0, b4 = 0;
+                if (e2 >= rlo && e2 + 8u <= fill) {
+                    lo32 = ring4(S, e2);
+                    b4 = ring4(S, e2 + 4u);
+                } else if (e2 + 8u <= un) {
+                    uint2 t;
+                    __builtin_memcpy(&t, in + e2, 8);
+                    lo32 = t.x;
+                    b4 = t.y;
+                } else {
+                    for (uint32_t t = 0; t < 5u; t++) {
+                        const uint32_t by = in[e2 + t];
+                        if (t < 4) lo32 |= by << (8 * t); else b4 = by;
                     }
                 }
-                ex = (entry < seg_hi) ? p : entry;
-                const uint32_t prev = wave_shr1(wave_incl_max(unknown ? 0u : ex), 0u);
-                const uint32_t ne = prev > floor_e ? prev : floor_e;
-                const bool bad = (ne != entry) || unknown;
-                entry = ne;
-                const unsigned long long bm = __ballot(bad);
-                if (!bm) break;
-                conf = __ffsll((long long)bm);  // first bad walker's new entry is exact
-            }
-            STAT(4);
-            STAT_ADD(9, it_done);
-            // anchors: max of earlier walkers' last match ends (and the carried one)
-            const uint32_t carry_a = S.carry_a;
-            const uint32_t incl = wave_incl_max(last_end);
-            const uint32_t excl = wave_shr1(incl, 0u);
-            const uint32_t anchor_in = excl > carry_a ? excl : carry_a;
-            uint32_t bytes = rest;
-            if (first_m != 0xFFFFFFFFu) {
-                const uint32_t lit = first_m - anchor_in;
-                bytes += ext_bytes(lit) + lit;
-            }
-            const uint32_t o0 = S.cursor + wave_excl_scan(bytes);
-            const uint32_t total = lane_val(o0 + bytes, 63);
-            S.seg_entry[lane] = entry;
-            S.seg_anchor[lane] = anchor_in;
-            S.seg_out[lane] = o0;
-            STAT(5);
-            if (lane == 63) {
-                S.carry_p = ex;
-                S.carry_a = incl > carry_a ? incl : carry_a;
-                S.cursor = total;
-                if (total + 16 > (uint32_t)kOutCap) S.overflow = 1;  // keep room for the tail
+                wave_sync();
+                S.tab[hash5(lo32, b4)] = (uint16_t)e2;
             }
         }
-        __syncthreads();
-        // ---- E: emission by all 8 waves: 8 threads per walker segment; thread k
-        // writes the k-th sequence (a segment holds <= 8), the 8 share long literals
-        if (parse_round && !S.overflow) {
-            const int l = tid >> 3, k = tid & 7;
-            const uint32_t seg_lo = R0 + l * kSegE, seg_hi = seg_lo + kSegE;
-            const uint32_t mword = S.mask[l];
-            uint32_t p = S.seg_entry[l], an = S.seg_anchor[l], o = S.seg_out[l];
-            for (int i = 0; p < seg_hi; i++) {
-                const uint32_t w = mword & (0xFFFFFFFFu << (p - seg_lo));
-                if (!w) break;
-                const uint32_t m = seg_lo + __builtin_ctz(w);
-                const uint32_t v = S.info[m - R0];
-                const uint32_t len = v >> 16, off = v & 0xFFFFu;
-                const uint32_t lit = m - an, ml = len - 4;
-                const uint32_t hdr = 1 + ext_bytes(lit);
-                if (i == k) {
-                    out[o] = (uint8_t)(((lit < 15 ? lit : 15) << 4) | (ml < 15 ? ml : 15));
-                    put_len(out + o + 1, lit);
-                    uint8_t *q = out + o + hdr + lit;
-                    q[0] = (uint8_t)off;
-                    q[1] = (uint8_t)(off >> 8);
-                    put_len(q + 2, ml);
-                    if (lit <= (uint32_t)kLongLit)
-                        for (uint32_t t = 0; t < lit; t++) out[o + hdr + t] = S.in[an + t];
+        wave_sync();
+        STAT(2);
+
+        // ---- 4. emission ----
+        if (members) {
+            const uint32_t ms = p - m_back;              // match start after catch-up
+            const uint32_t end = ms + m_len;
+            const uint32_t an = umax(wave_shr1(wave_incl_max(mem ? end : 0u), 0u), anchor0);
+            const uint32_t lit = mem ? ms - an : 0u;
+            const uint32_t ml = m_len - kMinMatch;
+            const uint32_t hdr = 1u + ext_bytes(lit);
+            const uint32_t size = mem ? hdr + lit + 2u + ext_bytes(ml) : 0u;
+            const uint32_t ex = wave_excl_scan(size);
+            const uint32_t tot = lane_val(ex + size, 63);
+            if ((uint64_t)o + tot > cap) {
+                overflow = true;
+                break;
+            }
+            const uint32_t ol = o + ex;
+            if (mem) {
+                uint8_t *d = dst + ol;
+                d[0] = (uint8_t)(((lit < 15u ? lit : 15u) << 4) | (ml < 15u ? ml : 15u));
+                put_len(d + 1, lit);
+                if (lit <= kLongLit) {
+                    // exact-length copy: whole dwords, then the tail bytes
+                    uint32_t k = 0;
+                    const bool inring = an >= rlo;   // an + lit <= fill always
+                    for (; k + 4u <= lit; k += 4u) {
+                        uint32_t v;
+                        if (inring) v = ring4(S, an + k);
+                        else __builtin_memcpy(&v, in + an + k, 4);
+                        __builtin_memcpy(d + hdr + k, &v, 4);
+                    }
+                    if (k < lit) {
+                        uint32_t v;
+                        if (inring) v = ring4(S, an + k);
+                        else { v = 0; for (uint32_t t = 0; k + t < lit; t++) v |= (uint32_t)in[an + k + t] << (8 * t); }
+                        for (; k < lit; k++, v >>= 8) d[hdr + k] = (uint8_t)v;
+                    }
                 }
-                if (lit > (uint32_t)kLongLit)  // all 8 threads of the segment
-                    for (uint32_t t = k; t < lit; t += 8) out[o + hdr + t] = S.in[an + t];
-                o += hdr + lit + 2 + ext_bytes(ml);
-                p = an = m + len;
+                const uint32_t off = p - c;
+                uint8_t *t = d + hdr + lit;
+                t[0] = (uint8_t)off;
+                t[1] = (uint8_t)(off >> 8);
+                put_len(t + 2, ml);
             }
+            // long literal runs: the whole wave copies them, one member at a time
+            uint64_t longm = __ballot(mem && lit > kLongLit);
+            while (longm) {
+                const int l = __builtin_ctzll(longm);
+                longm &= longm - 1ull;
+                const uint32_t la = lane_val(an, l), ll = lane_val(lit, l);
+                const uint32_t lo = lane_val(ol + hdr, l);
+                wave_copy(in, dst, la, lo, ll, lane);
+            }
+            o += tot;
+            STAT_ADD(11, __popcll(members));
         }
-        STAT(6);
-        __syncthreads();
-        STAT(7);
+        if (refill) {
+            wave_sync();
+            chunk_store(S, fill, lane, pre);
+            fill += kChunkE;
+            rlo = umax(rlo, fill - kRingE);
+        }
+        STAT(3);
         STAT_ADD(10, 1);
-        if (S.overflow) break;
+        P = q;
     }
 
-    // ---- last literals (:732-751) and flush ----
-    if (S.overflow) {
-        if (tid == 0) a.result[b] = 0;
-        return;
+    // ---- last literals (:732-751) ----
+    if (!overflow) {
+        const uint32_t lit = un - anchor;
+        const uint32_t hdr = 1u + ext_bytes(lit);
+        const uint32_t total = o + hdr + lit;
+        if (total > cap) {
+            overflow = true;
+        } else {
+            if (lane == 0) {
+                dst[o] = (uint8_t)((lit < 15u ? lit : 15u) << 4);
+                put_len(dst + o + 1, lit);
+            }
+            wave_copy(in, dst, anchor, o + hdr, lit, lane);
+            o = total;
+        }
     }
-    const uint32_t an = S.carry_a;
-    const uint32_t lit = (uint32_t)n - an;
-    uint32_t o = S.cursor;
-    const uint32_t hdr = 1 + ext_bytes(lit);
-    if (tid == 0) {
-        out[o] = (uint8_t)((lit < 15 ? lit : 15) << 4);
-        put_len(out + o + 1, lit);
-    }
-    o += hdr;
-    if (o + lit <= (uint32_t)kOutCap)
-        for (uint32_t k = tid; k < lit; k += kThreads) out[o + k] = S.in[an + k];
-    __syncthreads();
-    const uint32_t total = o + lit;
-    if (total > (uint32_t)kOutCap) {  // cannot happen (output <= compressBound)
-        if (tid == 0) a.result[b] = 0;
-        return;
-    }
-    if (tid == 0) a.result[b] = (total <= (uint32_t)cap) ? (int)total : 0;
-    if (total <= (uint32_t)cap) {
-        const uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15);
-        const uint32_t hh = head < total ? head : total;
-        if ((uint32_t)tid < hh) dst[tid] = out[tid];
-        const uint32_t body = (total - hh) & ~15u;
-        for (uint32_t k = hh + 16 * tid; k < hh + body; k += 16 * kThreads)
-            *(uint4 *)(dst + k) = *(const uint4 *)(out + k);
-        for (uint32_t k = hh + body + tid; k < total; k += kThreads) dst[k] = out[k];
-    }
-    STAT(8);
-    STAT_ADD(11, 1);
+    if (lane == 0) a.result[b] = overflow ? 0 : (int)o;
+    STAT(4);
+    STAT_ADD(13, 1);
     STATS_FLUSH(g_enc_stats);
 }
 
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(lz4_encode_kernel, dim3(a.nblocks), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(lz4_encode_kernel, dim3(a.nblocks), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -40,6 +40,7 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
 }
 
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
     x = umax(x, dpp<kDppRowShr1>(0u, x));

@@ -1,0 +1,254 @@
+/* enc_model.c -- DESIGN TOOL (not product, not oracle): CPU model of candidate
+ * policies for a round-parallel LZ4 match finder, to compare compression ratio
+ * against the reference encoder before committing a GPU design.
+ *
+ *   gcc -O2 -o /tmp/enc_model tools/enc_model.c oracle/synth.c && /tmp/enc_model
+ *
+ * Policies (all greedy parses, valid LZ4 limits: match start <= n-12, end <= n-5):
+ *   insert = 0: every position inserted (hash -> latest earlier position)
+ *   insert = 1: only walked positions (literal positions + match starts) and
+ *               match_end - 2, as the reference does
+ *   rounds R:   lookups during round [R0, R0+R) see only insertions of earlier rounds
+ *   inround:    also try the earliest same-hash position inside the round
+ *   back:       backward match extension into pending literals (reference catch-up)
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+void synth_blocks(uint8_t *out, int n, long long stride, long long first, int nb, int kind);
+
+static uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static uint64_t rd64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
+
+static int ext(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
+
+static long model(const uint8_t *in, int n, int hlog, int insert, int R, int inround, int back)
+{
+    const int H = 1 << hlog;
+    int *tab = malloc(sizeof(int) * H);
+    for (int i = 0; i < H; i++) tab[i] = -1;
+    int *cand = malloc(sizeof(int) * n), *cand2 = malloc(sizeof(int) * n);
+    uint32_t *hh = malloc(sizeof(uint32_t) * n);
+    const int mstart = n - 12, mlimit = n - 5;
+    long out = 0;
+    int anchor = 0, p = 0;
+    for (int r0 = 0; r0 < n; r0 += R) {
+        int r1 = r0 + R < n ? r0 + R : n;
+        for (int q = r0; q < r1; q++) {
+            if (q + 8 <= n) hh[q] = (uint32_t)((rd64(in + q) * 889523592379ULL) >> (40 - hlog)) & (H - 1);
+            else hh[q] = 0;
+            cand[q] = (q <= n - 5) ? tab[hh[q]] : -1;
+            cand2[q] = -1;
+        }
+        if (inround) {
+            for (int q = r0; q < r1 && q <= n - 5; q++) {
+                for (int j = r0; j < q; j++)
+                    if (hh[j] == hh[q]) { cand2[q] = j; break; }
+            }
+        }
+        if (insert == 0)
+            for (int q = r0; q < r1 && q <= n - 5; q++) tab[hh[q]] = q;
+        /* walk this round */
+        while (p < r1) {
+            int best = 0, bc = -1;
+            if (p >= 1 && p <= mstart) {
+                int cs[2] = {cand[p], cand2[p]};
+                for (int k = 0; k < 2; k++) {
+                    int c = cs[k];
+                    if (c < 0 || c >= p || p - c > 65535) continue;
+                    if (rd32(in + c) != rd32(in + p)) continue;
+                    int l = 4;
+                    while (p + l < mlimit && in[p + l] == in[c + l]) l++;
+                    if (l > best || (l == best && c > bc)) { best = l; bc = c; }
+                }
+            }
+            if (insert == 1 && p <= n - 5) tab[hh[p]] = p; /* walked position */
+            if (best >= 4) {
+                int m = p, c = bc, len = best;
+                if (back)
+                    while (m > anchor && c > 0 && in[m - 1] == in[c - 1]) { m--; c--; len++; }
+                int lit = m - anchor;
+                out += 1 + ext(lit) + lit + 2 + ext(len - 4);
+                p = m + len;
+                anchor = p;
+                if (insert == 1 && p - 2 <= n - 5) tab[hh[p - 2] = (uint32_t)((rd64(in + p - 2) * 889523592379ULL) >> (40 - hlog)) & (H - 1)] = p - 2;
+            } else {
+                p++;
+            }
+        }
+    }
+    int lit = n - anchor;
+    out += 1 + ext(lit) + lit;
+    free(tab); free(cand); free(cand2); free(hh);
+    return out;
+}
+
+
+/* Wave-per-block policy: rounds of R positions start at the walk position P;
+ * lookups see the table as of the round start (walked positions + end-2 of
+ * earlier rounds); in-round candidate = earliest lane with the same low `sb`
+ * hash bits; backward extension capped at `bcap` bytes. */
+static long model2(const uint8_t *in, int n, int hlog, int R, int sb, int bcap, int end2)
+{
+    const int H = 1 << hlog;
+    int *tab = calloc(H, sizeof(int));
+    int *cand = malloc(sizeof(int) * (R + 1)), *cand2 = malloc(sizeof(int) * (R + 1));
+    uint32_t *hh = malloc(sizeof(uint32_t) * (R + 1));
+    int *scr = malloc(sizeof(int) * (1 << sb));
+    const int mstart = n - 12, mlimit = n - 5;
+    long out = 0;
+    int anchor = 0, p = 0;
+    while (p < n) {
+        const int P = p, r1 = P + R < n ? P + R : n;
+        for (int i = 0; i < (1 << sb); i++) scr[i] = -1;
+        for (int q = P; q < r1; q++) {
+            hh[q - P] = (q + 8 <= n) ? (uint32_t)((rd64(in + q) * 889523592379ULL) >> (40 - hlog)) & (H - 1) : 0;
+            cand[q - P] = tab[hh[q - P]];
+            int k = hh[q - P] & ((1 << sb) - 1);
+            cand2[q - P] = -1;
+            if (scr[k] < 0) scr[k] = q; else cand2[q - P] = scr[k];
+        }
+        int walked[4096]; int nw = 0; int ends[4096]; int ne = 0;
+        while (p < r1) {
+            int best = 0, bc = -1;
+            if (p >= 1 && p <= mstart) {
+                int cs[2] = {cand[p - P], cand2[p - P]};
+                for (int k = 0; k < 2; k++) {
+                    int c = cs[k];
+                    if (c < 0 || c >= p || p - c > 65535) continue;
+                    if (rd32(in + c) != rd32(in + p)) continue;
+                    int l = 4;
+                    while (p + l < mlimit && in[p + l] == in[c + l]) l++;
+                    if (l > best || (l == best && c > bc)) { best = l; bc = c; }
+                }
+            }
+            walked[nw++] = p;
+            if (best >= 4) {
+                int m = p, c = bc, len = best, b = 0;
+                while (b < bcap && m > anchor && c > 0 && in[m - 1] == in[c - 1]) { m--; c--; len++; b++; }
+                int lit = m - anchor;
+                out += 1 + ext(lit) + lit + 2 + ext(len - 4);
+                p = m + len;
+                anchor = p;
+                ends[ne++] = p - 2;
+            } else {
+                p++;
+            }
+        }
+        for (int i = 0; i < nw; i++) if (walked[i] <= n - 5 && walked[i] < r1) tab[hh[walked[i] - P]] = walked[i];
+        if (end2) for (int i = 0; i < ne; i++) if (ends[i] + 8 <= n) tab[(uint32_t)((rd64(in + ends[i]) * 889523592379ULL) >> (40 - hlog)) & (H - 1)] = ends[i];
+    }
+    int lit = n - anchor;
+    out += 1 + ext(lit) + lit;
+    free(tab); free(cand); free(cand2); free(hh); free(scr);
+    return out;
+}
+
+/* Producer/consumer policy: every position inserted (latest earlier position
+ * with the same hash), chunks of R positions see the table as of the chunk
+ * start (plus `lag` chunks of staleness for parallel producers), in-round
+ * candidate = earliest lane with the same low `sb` hash bits, back-ext cap. */
+static long model3(const uint8_t *in, int n, int hlog, int R, int lag, int sb, int bcap)
+{
+    const int H = 1 << hlog;
+    int *tab = calloc(H, sizeof(int));
+    int *cand = malloc(sizeof(int) * n), *cand2 = malloc(sizeof(int) * n);
+    uint32_t *hh = malloc(sizeof(uint32_t) * n);
+    int *scr = malloc(sizeof(int) * (1 << sb));
+    for (int q = 0; q < n; q++)
+        hh[q] = (q + 8 <= n) ? (uint32_t)((rd64(in + q) * 889523592379ULL) >> (40 - hlog)) & (H - 1) : 0;
+    /* candidates per chunk: table state after chunks < k - lag */
+    int done = 0;  /* positions inserted so far */
+    for (int r0 = 0; r0 < n; r0 += R) {
+        int lim = r0 - lag * R;
+        for (; done < lim; done++) if (done <= n - 5) tab[hh[done]] = done;
+        int r1 = r0 + R < n ? r0 + R : n;
+        for (int i = 0; i < (1 << sb); i++) scr[i] = -1;
+        for (int q = r0; q < r1; q++) {
+            cand[q] = (q <= n - 5) ? tab[hh[q]] : -1;
+            int k = hh[q] & ((1 << sb) - 1);
+            cand2[q] = -1;
+            if (scr[k] < 0) scr[k] = q; else cand2[q] = scr[k];
+        }
+    }
+    const int mstart = n - 12, mlimit = n - 5;
+    long out = 0;
+    int anchor = 0, p = 0;
+    while (p < n) {
+        int best = 0, bc = -1;
+        if (p >= 1 && p <= mstart) {
+            int cs[2] = {cand[p], cand2[p]};
+            for (int k = 0; k < 2; k++) {
+                int c = cs[k];
+                if (c < 0 || c >= p || p - c > 65535) continue;
+                if (rd32(in + c) != rd32(in + p)) continue;
+                int l = 4;
+                while (p + l < mlimit && in[p + l] == in[c + l]) l++;
+                if (l > best || (l == best && c > bc)) { best = l; bc = c; }
+            }
+        }
+        if (best >= 4) {
+            int m = p, c = bc, len = best, b = 0;
+            while (b < bcap && m > anchor && c > 0 && in[m - 1] == in[c - 1]) { m--; c--; len++; b++; }
+            int lit = m - anchor;
+            out += 1 + ext(lit) + lit + 2 + ext(len - 4);
+            p = m + len;
+            anchor = p;
+        } else p++;
+    }
+    int lit = n - anchor;
+    out += 1 + ext(lit) + lit;
+    free(tab); free(cand); free(cand2); free(hh); free(scr);
+    return out;
+}
+
+int main(int argc, char **argv)
+{
+    const int n = 65536, nb = argc > 1 ? atoi(argv[1]) : 16;
+    uint8_t *buf = malloc((size_t)n * nb + 16);
+    synth_blocks(buf, n, n, 0, nb, 1);
+    struct { int hlog, insert, R, inround, back; const char *name; } P[] = {
+        {12, 0, 2048, 1, 0, "current: 4096, all positions, 2048 rounds, in-round"},
+        {13, 0, 2048, 1, 0, "8192, all positions, 2048 rounds, in-round"},
+        {13, 1, 1, 0, 0, "8192, walked only, sequential (ref-like)"},
+        {13, 1, 1, 0, 1, "8192, walked only, sequential, back-ext (ref-like)"},
+        {13, 1, 64, 0, 1, "8192, walked only, 64 rounds, back-ext"},
+        {13, 1, 64, 1, 1, "8192, walked only, 64 rounds, in-round, back-ext"},
+        {12, 1, 64, 1, 1, "4096, walked only, 64 rounds, in-round, back-ext"},
+        {13, 1, 256, 1, 1, "8192, walked only, 256 rounds, in-round, back-ext"},
+        {13, 1, 2048, 1, 1, "8192, walked only, 2048 rounds, in-round, back-ext"},
+        {12, 0, 2048, 1, 1, "4096, all positions, 2048 rounds, in-round, back-ext"},
+        {13, 0, 2048, 1, 1, "8192, all positions, 2048 rounds, in-round, back-ext"},
+        {14, 0, 2048, 1, 1, "16384, all positions, 2048 rounds, in-round, back-ext"},
+    };
+    for (unsigned k = 0; k < sizeof(P) / sizeof(P[0]); k++) {
+        long tot = 0;
+        for (int b = 0; b < nb; b++)
+            tot += model(buf + (size_t)b * n, n, P[k].hlog, P[k].insert, P[k].R, P[k].inround, P[k].back);
+        printf("%-62s ratio %.4f\n", P[k].name, (double)n * nb / tot);
+    }
+    struct { int hlog, R, sb, bcap, end2; } Q[] = {
+        {13, 64, 8, 4, 1}, {13, 64, 8, 4, 0}, {13, 64, 8, 0, 1}, {13, 64, 8, 64, 1}, {13, 64, 0, 4, 1},
+        {12, 64, 8, 4, 1}, {13, 128, 8, 4, 1}, {13, 64, 6, 4, 1}, {14, 64, 8, 4, 1}};
+    for (unsigned k = 0; k < sizeof(Q) / sizeof(Q[0]); k++) {
+        long tot = 0;
+        for (int b = 0; b < nb; b++)
+            tot += model2(buf + (size_t)b * n, n, Q[k].hlog, Q[k].R, Q[k].sb, Q[k].bcap, Q[k].end2);
+        printf("wave: hlog %d R %d scratch-bits %d back-cap %d end-2 %d        ratio %.4f\n", Q[k].hlog,
+               Q[k].R, Q[k].sb, Q[k].bcap, Q[k].end2, (double)n * nb / tot);
+    }
+    struct { int hlog, R, lag, sb, bcap; } T3[] = {
+        {13, 64, 0, 8, 4}, {13, 64, 1, 8, 4}, {13, 64, 2, 8, 4}, {12, 64, 0, 8, 4}, {12, 64, 1, 8, 4},
+        {13, 64, 0, 8, 64}, {13, 64, 0, 6, 4}, {14, 64, 1, 8, 4}, {12, 128, 0, 8, 4}};
+    for (unsigned k = 0; k < sizeof(T3) / sizeof(T3[0]); k++) {
+        long tot = 0;
+        for (int b = 0; b < nb; b++)
+            tot += model3(buf + (size_t)b * n, n, T3[k].hlog, T3[k].R, T3[k].lag, T3[k].sb, T3[k].bcap);
+        printf("prod/cons: hlog %d R %d lag %d scratch-bits %d back-cap %d       ratio %.4f\n", T3[k].hlog,
+               T3[k].R, T3[k].lag, T3[k].sb, T3[k].bcap, (double)n * nb / tot);
+    }
+    free(buf);
+    return 0;
+}

@@ -10,14 +10,13 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["APE_LZ4_LIB"] = os.path.join(ROOT, "libapenetwork_amd", "libape_lz4_amd_stats.so")
+os.environ.setdefault("APE_LZ4_LIB", os.path.join(ROOT, "libapenetwork_amd", "libape_lz4_amd_stats.so"))
 sys.path.insert(0, ROOT)
 
 DEC = ["parse", "copy", "(batches)", "(steps)", "(restages)", "", "", "", "", "", "(blocks)", "", "", "",
        "", ""]
-ENC = ["load+init", "A hash+min", "B read", "C roll+verify", "D fixpoint", "D sizes", "E emit",
-       "E deferred+barrier", "last+flush", "(fixpoint iters)", "(rounds)", "(blocks)", "", "", "",
-       ""]
+ENC = ["candidates", "walk", "table", "emit", "last", "", "", "", "", "", "(rounds)",
+       "(members)", "(extensions)", "(blocks)", "", ""]
 
 
 def main():
@@ -51,7 +50,7 @@ def main():
         L.APE_LZ4_debug_stats(which, buf, 1)
         ms = e0.elapsed_time(e1)
         vals = list(buf)
-        blocks = vals[11] if which else vals[10]
+        blocks = vals[labels.index("(blocks)")]
         print("%s: %d blocks, %.2f ms, %.1f GB/s (in+out bytes)" % (
             name, nb, ms, (nb * n + int(csz.sum())) / ms / 1e6))
         tot = sum(v for i, v in enumerate(vals) if labels[i] and not labels[i].startswith("(") and labels[i] != "-")
