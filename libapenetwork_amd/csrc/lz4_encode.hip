@@ -4,35 +4,52 @@
 // 811-815 -> LZ4_compress_generic :530-755, byU16 / noDict).  The output is a
 // valid LZ4 v1.7.1 block -- it obeys every parsing rule decompress_safe enforces
 // (:1346-1366, :1375, :1444-1447): matches start at <= n-12, end at <= n-5, the
-// last >= 5 bytes are literals -- but it is produced by a round-parallel parse,
+// last >= 5 bytes are literals -- but it is produced by a chunk-parallel parse,
 // not by the reference's sequential search, so the bytes differ.
 //
-// One wave (one 64-thread workgroup) per block.  A batch holds ~1M blocks, so
-// the parallelism comes from many blocks in flight; per wave the LDS holds only
-// the reference's own hash table (8192 x u16, 13-bit hash of 5 bytes, :449-462)
-// plus a 1 KiB scratch, ~17 KiB, so 9 blocks share a CU.  The input stays in
-// HBM/L2 and is read with unaligned 16-byte loads.
+// One 128-thread workgroup (two waves) per block; a batch holds ~1M blocks, so
+// most of the parallelism comes from many blocks in flight.  Per block the LDS
+// holds the reference's own hash table (8192 x u16, 13-bit hash of 5 bytes,
+// :449-462), a 4 KiB ring of recent input and two chunks of match info (~22 KiB,
+// 7 blocks per CU).  The input stays in HBM/L2, read with unaligned 16-byte loads.
 //
-// The block is parsed in rounds of 64 positions starting at the parse position P:
-//  1. every lane p = P + lane loads in[p-4, p+28), hashes in[p, p+5) and reads
-//     two candidates: T = table[h] (positions walked in earlier rounds, as the
-//     reference inserts them: :595-619, :680-706) and L = the earliest lane of
-//     this round with the same low hash bits (found with an LDS atomicMin);
-//     it loads in[c-4, c+28) for both, verifies 4 bytes, measures the match up
-//     to 28 bytes and how far it extends backwards (up to 4 bytes);
-//  2. the scalar unit walks the greedy chain through the round: jump to the
-//     next lane with a match (ballot mask), extend it backwards into pending
-//     literals (the reference's catch-up, :628-629) and, for a match that
-//     reached 28 bytes, forwards with the whole wave (1 KiB per step);
-//  3. walked positions and match_end - 2 (:680) go into the table;
-//  4. member lanes emit their sequences straight to dst (prefix sums give the
-//     offsets), a literal run longer than 32 bytes is copied by the whole wave.
-// Last literals (:732-751) are copied by the whole wave with 16-byte moves.
-#include <string.h>
-
+// The block is cut into chunks of 64 positions.  The two waves split the work
+// so that each waits only on its own memory operations (s_waitcnt vmcnt counts a
+// wave's loads and stores together, in order):
+//   PRODUCER (wave 1), software-pipelined one chunk ahead of the consumer:
+//     A(k+2)  load in[p-4, p+28) for every position p of chunk k+2;
+//     B(k+1)  hash in[p, p+5), read candidate T = table[h] (positions walked
+//             earlier, inserted as the reference does: :595-619, :680-706) and
+//             L = the earliest lane of the chunk with the same low hash bits;
+//             issue the load of in[T-4, T+28); copy the chunk into the ring;
+//     C(k)    verify 4 bytes for T and L, measure up to 28 bytes forward and
+//             4 backward, keep the longer (then closer) -> match info in LDS.
+//   CONSUMER (wave 0), one chunk behind:
+//     walk    the greedy chain through chunk k-1 on the scalar unit: jump to the
+//             next lane with a match (ballot mask), catch up backwards into
+//             pending literals (:623-627), extend a match that reached 28 bytes
+//             with the whole wave (1 KiB per step);
+//     table   insert the walked positions and match_end - 2 (:680);
+//     emit    member lanes write their sequences straight to dst (prefix sums
+//             give the offsets); long literal runs and the last literals
+//             (:732-751) are copied by the whole wave with 16-byte moves.
+//   Two workgroup barriers per step keep the table reads of B (before the first)
+//   apart from the consumer's inserts (after it), so the output is deterministic.
 #include "lz4_gpu_internal.h"
 
 namespace apelz4 {
+
+#ifdef APE_LZ4_STATS
+__device__ unsigned long long g_enc_stats[16];
+hipError_t enc_stats_read(unsigned long long *out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_enc_stats), sizeof(g_enc_stats));
+    if (e == hipSuccess && reset) {
+        unsigned long long z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_enc_stats), z, sizeof(z));
+    }
+    return e;
+}
+#endif
 
 namespace {
 
@@ -41,90 +58,93 @@ namespace {
 #endif
 constexpr int kHLog = APE_LZ4_HLOG;
 constexpr int kHSize = 1 << kHLog;
-constexpr uint32_t kEagerLen = 28;   // match bytes measured before the walk
+constexpr uint32_t kEagerLen = 28;   // match bytes measured by the producer
 constexpr uint32_t kLongLit = 32;    // longer literal runs are copied by the wave
-#ifndef APE_LZ4_ERING
-#define APE_LZ4_ERING 8192
-#endif
-constexpr uint32_t kRingE = APE_LZ4_ERING;  // per-wave ring of recent input bytes
-constexpr uint32_t kChunkE = 512;    // ring refill granule (8 bytes per lane)
-constexpr uint32_t kAhead = 1024;    // keep the ring filled this far past P
+constexpr uint32_t kRingE = 4096;    // recent input bytes for the consumer
+constexpr int kSmall = 128;          // smaller blocks take the byte-load path
+
+constexpr uint32_t kEager2 = kEagerLen + 32;  // after the producer's second stage
+
+// info.x: len (8) | back << 8 (3) | trunc << 11 | has << 12 | hashable << 13 |
+//         e2 << 14 | hash(match_end - 2) << 16;   info.y: offset | h << 16
+constexpr uint32_t I_TRUNC = 1u << 11, I_HAS = 1u << 12, I_HASHABLE = 1u << 13,
+                   I_E2 = 1u << 14;
 
 struct __attribute__((aligned(16))) EncLds {
     uint16_t tab[kHSize];
-    uint32_t scr[256];
     uint32_t ring[kRingE / 4];       // input byte x at ring byte (x mod kRingE)
+    uint2 info[2][64];
+    uint32_t scr[256];               // producer scratch: earliest lane per low hash bits
 };
 
-// Compiler barrier for lane-to-lane communication through LDS inside one wave.
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// 32 bytes in[pos, pos+32) as 8 dwords; bytes outside [0, n) read as 0.
-__device__ __forceinline__ void ld32b(const uint8_t *in, int n, int pos, uint32_t (&X)[8]) {
-    if (pos >= 0 && pos + 32 <= n) {
-        uint4 a, b;
-        __builtin_memcpy(&a, in + pos, 16);
-        __builtin_memcpy(&b, in + pos + 16, 16);
-        X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w;
-        X[4] = b.x; X[5] = b.y; X[6] = b.z; X[7] = b.w;
-    } else {
+// X = L shifted by d bytes (X byte i = L byte i + d, 0 outside L), |d| < 32,
+// with compile-time register indices only (a barrel shifter).
+__device__ __forceinline__ void shift_bytes(const uint32_t (&L)[8], int d, uint32_t (&X)[8]) {
+    uint32_t T[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) T[k] = L[k];
+    const bool down = d >= 0;
+    const int ad = down ? d : -d, w = ad >> 2;
+    const uint32_t r = (uint32_t)ad & 3u;
+#pragma unroll
+    for (int bit = 4; bit >= 1; bit >>= 1) {
+        if (w & bit) {
+            if (down) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) T[k] = (k + bit < 8) ? T[k + bit] : 0u;
+            } else {
+#pragma unroll
+                for (int k = 7; k >= 0; k--) T[k] = (k - bit >= 0) ? T[k - bit] : 0u;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (down) X[k] = __builtin_amdgcn_alignbyte(k + 1 < 8 ? T[k + 1] : 0u, T[k], r);
+        else X[k] = r ? __builtin_amdgcn_alignbyte(T[k], k >= 1 ? T[k - 1] : 0u, 4u - r) : T[k];
+    }
+}
+
+// 32 bytes in[pos, pos+32) (bytes outside [0, n) read as 0).
+// SMALL: byte loads.  Otherwise (n >= 32): two unaligned 16-byte loads from the
+// clamped window, fixed up with ALU only (so the wave's vmcnt accounting stays
+// static in the pipelined loop).
+template <bool SMALL>
+__device__ __forceinline__ void load32(const uint8_t *in, int n, int pos, uint32_t (&X)[8]) {
+    if (SMALL) {
 #pragma unroll
         for (int k = 0; k < 8; k++) X[k] = 0;
+#pragma unroll
         for (int k = 0; k < 32; k++) {
             const int q = pos + k;
             if (q >= 0 && q < n) X[k >> 2] |= (uint32_t)in[q] << (8 * (k & 3));
         }
+        return;
     }
-}
-
-// 8 input bytes at a (zero beyond n): one ring refill lane
-__device__ __forceinline__ uint2 chunk_load(const uint8_t *in, uint32_t n, uint32_t a) {
-    uint2 v = make_uint2(0u, 0u);
-    if (a + 8u <= n) {
-        __builtin_memcpy(&v, in + a, 8);
+    const int ca = pos < 0 ? 0 : (pos > n - 32 ? n - 32 : pos);
+    uint4 a, b;
+    __builtin_memcpy(&a, in + ca, 16);
+    __builtin_memcpy(&b, in + ca + 16, 16);
+    const uint32_t L[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    if (ca == pos) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) X[k] = L[k];
     } else {
-        for (uint32_t t = 0; t < 8u && a + t < n; t++) {
-            const uint32_t by = (uint32_t)in[a + t] << (8 * (t & 3));
-            if (t < 4) v.x |= by; else v.y |= by;
+        // the clamped window ends at n / starts at 0, so shifting it zero-fills
+        // exactly the bytes outside [0, n)
+        const int d = pos - ca;   // |d| >= 32 only for lanes past the block end
+        shift_bytes(L, d < -31 ? -31 : (d > 31 ? 31 : d), X);
+        if (d > 31 || d < -31) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) X[k] = 0;
         }
     }
-    return v;
-}
-
-__device__ __forceinline__ void chunk_store(EncLds &S, uint32_t f, int lane, uint2 v) {
-    *(uint2 *)&S.ring[((f + 8u * (uint32_t)lane) & (kRingE - 1)) >> 2] = v;
-}
-
-// Fill the ring with [f0, f0 + 2*kChunkE) now (after a jump past the filled bytes).
-__device__ __forceinline__ void ring_fill(EncLds &S, const uint8_t *in, uint32_t n, uint32_t f0,
-                                          int lane) {
-    const uint2 a = chunk_load(in, n, f0 + 8u * (uint32_t)lane);
-    const uint2 b = chunk_load(in, n, f0 + kChunkE + 8u * (uint32_t)lane);
-    chunk_store(S, f0, lane, a);
-    chunk_store(S, f0 + kChunkE, lane, b);
-}
-
-// 32 bytes at pos from the ring (pos >= fill - kRingE, or pos < 0 while the
-// ring's tail is still zero)
-__device__ __forceinline__ void ring32(const EncLds &S, int pos, uint32_t (&X)[8]) {
-    const uint32_t sh = (uint32_t)pos & 3u;
-    const int w0 = pos >> 2;
-    uint32_t W[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) W[k] = S.ring[(uint32_t)(w0 + k) & (kRingE / 4 - 1)];
-#pragma unroll
-    for (int k = 0; k < 8; k++) X[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
-}
-
-// 4 input bytes at x from the ring
-__device__ __forceinline__ uint32_t ring4(const EncLds &S, uint32_t x) {
-    const uint32_t w = x >> 2;
-    return __builtin_amdgcn_alignbyte(S.ring[(w + 1) & (kRingE / 4 - 1)],
-                                      S.ring[w & (kRingE / 4 - 1)], x & 3u);
 }
 
 // the reference's hash of the 5 bytes at p (x1 = in[p..p+3], b4 = in[p+4])
@@ -154,14 +174,30 @@ __device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {  // bytes after a 15
     return v >= 15 ? (v - 15) / 255 + 1 : 0;
 }
 
-// write the length extension of v (>= 15) at o, returns bytes written
-__device__ __forceinline__ uint32_t put_len(uint8_t *o, uint32_t v) {
-    if (v < 15) return 0;
+// write the length extension of v (>= 15) at o
+__device__ __forceinline__ void put_len(uint8_t *o, uint32_t v) {
+    if (v < 15) return;
     v -= 15;
     uint32_t k = 0;
     for (; v >= 255; v -= 255) o[k++] = 255;
-    o[k++] = (uint8_t)v;
-    return k;
+    o[k] = (uint8_t)v;
+}
+
+// 4 input bytes at x from the ring
+__device__ __forceinline__ uint32_t ring4(const EncLds &S, uint32_t x) {
+    const uint32_t w = x >> 2;
+    return __builtin_amdgcn_alignbyte(S.ring[(w + 1) & (kRingE / 4 - 1)],
+                                      S.ring[w & (kRingE / 4 - 1)], x & 3u);
+}
+
+// 32 input bytes at x from the ring
+__device__ __forceinline__ void ring32(const EncLds &S, uint32_t x, uint32_t (&O)[8]) {
+    const uint32_t w0 = x >> 2, sh = x & 3u;
+    uint32_t W[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) W[k] = S.ring[(w0 + k) & (kRingE / 4 - 1)];
+#pragma unroll
+    for (int k = 0; k < 8; k++) O[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
 }
 
 // Copy in[a, a+len) to dst[o, o+len) with the whole wave (16 bytes per lane per step).
@@ -178,309 +214,397 @@ __device__ __forceinline__ void wave_copy(const uint8_t *in, uint8_t *dst, uint3
     }
 }
 
-}  // namespace
+struct Blk {
+    const uint8_t *in;
+    uint8_t *dst;
+    int n;
+    uint32_t un, cap, mstart, mlimit;
+    int nch;                         // chunks of 64 positions
+};
 
-#ifdef APE_LZ4_STATS
-__device__ unsigned long long g_enc_stats[16];
-hipError_t enc_stats_read(unsigned long long *out, int reset) {
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_enc_stats), sizeof(g_enc_stats));
-    if (e == hipSuccess && reset) {
-        unsigned long long z[16] = {0};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(g_enc_stats), z, sizeof(z));
-    }
-    return e;
+// ---------------- producer ----------------
+struct Part {                        // C1 result of one chunk, finished by C2
+    uint32_t len, c, bk, lim, h;
+    bool has, hashable, trunc1;
+};
+
+struct Prod {
+    uint32_t X1[8], X2[8], X3[8];    // own bytes of chunks s+1, s+2, s+3
+    uint32_t Y1[8], Y2[8];           // T-candidate bytes of chunks s+1, s+2
+    uint32_t E0[8], E1[8];           // second-stage candidate bytes of chunks s, s+1
+    uint32_t cT1, jL1, h1, cT2, jL2, h2;
+    Part q0, q1;
+};
+
+template <bool SMALL>
+__device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_t (&X)[8]) {
+    const int pos = (k < B.nch ? 64 * k : 0) + lane - 4;
+    load32<SMALL>(B.in, B.n, pos, X);
 }
-#endif
 
-__global__ void __launch_bounds__(64)
-lz4_encode_kernel(BlockArgs a) {
-    __shared__ EncLds S;
-    const int b = blockIdx.x;
-    const int lane = threadIdx.x;
-
-    const uint8_t *in =
-        (const uint8_t *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
-    uint8_t *dst = (uint8_t *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
-    const int n = a.src_size[b];
-    const uint32_t cap = (uint32_t)(a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride);
-    if (n < 0 || n > kMaxBlock) {
-        if (lane == 0) a.result[b] = n < 0 ? 0 : kErange;
-        return;
-    }
-    if ((int)cap < 0) {
-        if (lane == 0) a.result[b] = 0;
-        return;
-    }
-
-    STATS_DECL
-    // table = 0 (the reference's memset state: position 0 for every hash)
-    for (int i = lane; i < kHSize / 8; i += 64) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
-    for (int i = lane; i < 256; i += 64) S.scr[i] = 0xFFFFFFFFu;
-    for (int i = lane; i < (int)(kRingE / 16); i += 64) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
+// B(k): hash, table + in-chunk candidates, T fetch issue, ring copy
+template <bool SMALL>
+__device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int lane,
+                                            const uint32_t (&X)[8], uint32_t &cT, uint32_t &jL,
+                                            uint32_t &h, uint32_t (&Y)[8]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const bool live = k < B.nch;
+    const bool hashable = live && p + 5u <= B.un;
+    h = hash5(X[1], X[2]);
+    cT = S.tab[h];
+    const uint32_t hs = h & 255u;
+    if (hashable) atomicMin(&S.scr[hs], (uint32_t)lane);
     wave_sync();
-    uint32_t fill = 2 * kChunkE;  // ring holds input [rlo, fill)
-    uint32_t rlo = 0;
-    ring_fill(S, in, (uint32_t)n, 0u, lane);
+    jL = hashable ? S.scr[hs] : 0xFFFFFFFFu;
     wave_sync();
+    if (hashable) S.scr[hs] = 0xFFFFFFFFu;
+    // ring copy of this chunk (second-stage, match_end - 2 and literal source)
+    if (live && p < B.un) ((uint8_t *)S.ring)[p & (kRingE - 1)] = (uint8_t)X[1];
+    // T candidate bytes (issued now, consumed one step later)
+    const bool tryT = live && cT < p;
+    load32<SMALL>(B.in, B.n, tryT ? (int)cT - 4 : 0, Y);
+}
 
-    uint32_t anchor = 0;     // start of the pending literals (wave-uniform)
-    uint32_t o = 0;          // output cursor
-    bool overflow = false;
-    const uint32_t un = (uint32_t)n;
-    const uint32_t mstart = un >= 12 ? un - 12 : 0;   // matches start at <= n-12 (:585)
-    const uint32_t mlimit = un >= 5 ? un - 5 : 0;     // and end at <= n-5 (:633)
-    uint32_t P = 0;
-    if (n < kMinLength) P = un;                       // :584 -> last literals only
-
-    while (P < un && !overflow) {
-        // ---- 0. input ring: refill after a jump, prefetch the next chunk ----
-        if (fill < P + 96u) {
-            fill = (P >= 64u ? P - 64u : 0u) & ~7u;
-            rlo = fill;
-            wave_sync();
-            ring_fill(S, in, un, fill, lane);
-            fill += 2 * kChunkE;
-            wave_sync();
-        }
-        const bool refill = fill < P + kAhead;
-        uint2 pre = make_uint2(0u, 0u);
-        if (refill) pre = chunk_load(in, un, fill + 8u * (uint32_t)lane);
-
-        // ---- 1. candidates for p = P + lane ----
-        const uint32_t p = P + (uint32_t)lane;
-        uint32_t X[8];
-        ring32(S, (int)p - 4, X);
-        const bool hashable = p + 5 <= un;
-        const uint32_t h = hash5(X[1], X[2]);
-        const uint32_t cT = S.tab[h];
-        const uint32_t hs = h & 255u;
-        if (hashable) atomicMin(&S.scr[hs], (uint32_t)lane);
-        wave_sync();
-        const uint32_t jL = hashable ? S.scr[hs] : 0xFFFFFFFFu;
-        wave_sync();
-        if (hashable) S.scr[hs] = 0xFFFFFFFFu;
-        const bool can = p >= 1u && p <= mstart && n >= kMinLength;
-        const uint32_t cL = P + jL;
-        const bool tryT = can && cT < p;
-        const bool tryL = can && jL < (uint32_t)lane && cL != cT;
-        uint32_t Y[8], Z[8];
+// C1(k): verify / measure 28 bytes / pick; issue the second-stage load
+template <bool SMALL>
+__device__ __forceinline__ void prod_measure(const Blk &B, int k, int lane, const uint32_t (&X)[8],
+                                             const uint32_t (&Y)[8], uint32_t cT, uint32_t jL,
+                                             uint32_t h, Part &R, uint32_t (&E)[8]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const bool live = k < B.nch;
+    R.hashable = live && p + 5u <= B.un;
+    const bool can = live && p >= 1u && p <= B.mstart && B.n >= kMinLength;
+    const uint32_t cL = 64u * (uint32_t)k + jL;
+    uint32_t Z[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) { Y[k] = 0; Z[k] = 0; }
-        if (tryT) {
-            // recent candidates come from the ring, older ones from HBM / L2
-            if (cT >= rlo + 4u) ring32(S, (int)cT - 4, Y);
-            else ld32b(in, n, (int)cT - 4, Y);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) Z[k] = (uint32_t)__shfl((int)X[k], (int)(jL & 63u), 64);
-        if (!tryL) {
-#pragma unroll
-            for (int k = 0; k < 8; k++) Z[k] = 0;
-        }
-        const bool okT = tryT && Y[1] == X[1];
-        const bool okL = tryL && Z[1] == X[1];
-        const uint32_t lim = can ? mlimit - p : 0u;  // longest match allowed here
-        uint32_t lT = okT ? eager(X, Y) : 0u, lL = okL ? eager(X, Z) : 0u;
-        // a length that reached kEagerLen is "at least"; compare as such
-        const bool pickL = okL && (!okT || lL > lT || (lL == lT && cL > cT));
-        const uint32_t c = pickL ? cL : cT;
-        uint32_t len = pickL ? lL : lT;
-        const bool trunc = len >= kEagerLen && lim > kEagerLen;
-        if (len > lim) len = lim;
-        const uint32_t bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), c);  // c - back >= 0
-        const bool has = okT || okL;
-        // lane info: len (16) | back (3) << 16 | trunc << 19
-        const uint32_t info = len | (bk << 16) | (trunc ? (1u << 19) : 0u);
-        const uint64_t Mm = __ballot(has);
-        STAT(0);
+    for (int t = 0; t < 8; t++) Z[t] = (uint32_t)__shfl((int)X[t], (int)(jL & 63u), 64);
+    const bool okT = can && cT < p && Y[1] == X[1];
+    const bool okL = can && jL < (uint32_t)lane && cL != cT && Z[1] == X[1];
+    R.lim = can ? B.mlimit - p : 0u;
+    const uint32_t lT = okT ? eager(X, Y) : 0u, lL = okL ? eager(X, Z) : 0u;
+    const bool pickL = okL && (!okT || lL > lT || (lL == lT && cL > cT));
+    R.c = pickL ? cL : cT;
+    R.len = pickL ? lL : lT;
+    R.trunc1 = R.len >= kEagerLen && R.lim > kEagerLen;
+    if (R.len > R.lim) R.len = R.lim;
+    R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
+    R.has = okT || okL;
+    R.h = h;
+    load32<SMALL>(B.in, B.n, R.trunc1 ? (int)(R.c + kEagerLen) : 0, E);
+}
 
-        // ---- 2. greedy walk (scalar) ----
-        const uint32_t anchor0 = anchor;
-        uint32_t q = P;                 // walk position
-        uint64_t walked = 0, members = 0;
-        uint32_t m_back = 0, m_len = 0; // per member lane
-        for (;;) {
-            const uint32_t rel = q - P;
-            if (rel >= 64u) break;
-            const uint64_t w = Mm >> rel;
-            if (w == 0) {
-                walked |= ~0ull << rel;
-                q = P + 64u;
-                break;
-            }
-            const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
-            walked |= (~0ull << rel) & (j == 63 ? ~0ull : ((2ull << j) - 1ull));
-            const uint32_t v = lane_val(info, (int)j);
-            const uint32_t m = P + j;
-            uint32_t L = v & 0xFFFFu;
-            if (v & (1u << 19)) {
-                // forward extension with the whole wave, 1 KiB per step
-                const uint32_t cm = lane_val(c, (int)j);
-                const uint32_t lm = mlimit - m;
-                for (;;) {
-                    const uint32_t k = L + 16u * (uint32_t)lane;
-                    uint32_t d = 0;
-                    uint32_t at = 0;
-                    if (k < lm) {
+// C2(k): finish the truncated lengths against the ring, hash match_end - 2 -> info
+__device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int lane,
+                                            const Part &R, const uint32_t (&E)[8]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    uint32_t len = R.len;
+    bool trunc = false;
+    if (R.trunc1) {
+        uint32_t O[8];
+        ring32(S, p + kEagerLen, O);             // own bytes p+28 .. p+60
+        uint32_t ext = 32;
+#pragma unroll
+        for (int t = 7; t >= 0; t--) {
+            const uint32_t d = O[t] ^ E[t];
+            if (d) ext = 4u * (uint32_t)t + (__builtin_ctz(d) >> 3);
+        }
+        len = kEagerLen + ext;
+        trunc = ext == 32u && R.lim > kEager2;
+        if (len > R.lim) len = R.lim;
+    }
+    uint32_t e2 = 0;
+    if (R.has && !trunc) {
+        const uint32_t at = p + len - 2u;         // match end - 2 (:680)
+        if (at + 5u <= B.un) e2 = I_E2 | (hash5(ring4(S, at), ring4(S, at + 4u)) << 16);
+    }
+    S.info[k & 1][lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
+                                         (R.has ? I_HAS : 0u) | (R.hashable ? I_HASHABLE : 0u) | e2,
+                                     (R.has ? p - R.c : 0u) | (R.h << 16));
+}
+
+// ---------------- consumer ----------------
+struct Cons {
+    uint32_t q;          // walk position
+    uint32_t anchor;     // start of the pending literals
+    uint32_t o;          // output cursor
+    bool overflow;
+    uint64_t walked, members;
+    uint32_t m_back, m_len, anchor0;  // per member lane / at the step start
+};
+
+// first half: walk chunk k (no table writes)
+__device__ __forceinline__ void cons_walk(const EncLds &S, const Blk &B, int k, int lane, Cons &C) {
+    const uint32_t P = 64u * (uint32_t)k;
+    C.walked = 0;
+    C.members = 0;
+    C.anchor0 = C.anchor;
+    if (C.overflow || C.q >= P + 64u) return;
+    const uint2 iv = S.info[k & 1][lane];
+    const uint64_t Mm = __ballot((iv.x & I_HAS) != 0u);
+    uint32_t q = C.q;
+    for (;;) {
+        const uint32_t rel = q - P;
+        if (rel >= 64u) break;
+        const uint64_t w = Mm >> rel;
+        if (w == 0) {
+            C.walked |= ~0ull << rel;
+            q = P + 64u;
+            break;
+        }
+        const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
+        C.walked |= (~0ull << rel) & (j == 63 ? ~0ull : ((2ull << j) - 1ull));
+        const uint32_t v = lane_val(iv.x, (int)j);
+        const uint32_t m = P + j;
+        uint32_t L = v & 0xFFu;
+        if (v & I_TRUNC) {
+            // forward extension with the whole wave, 1 KiB per step
+            const uint32_t cm = m - (lane_val(iv.y, (int)j) & 0xFFFFu);
+            const uint32_t lm = B.mlimit - m;
+            for (;;) {
+                const uint32_t kk = L + 16u * (uint32_t)lane;
+                uint32_t d = 0, at = 0;
+                if (kk < lm) {
+                    uint32_t xb[4] = {0, 0, 0, 0}, yb[4] = {0, 0, 0, 0};
+                    if (m + kk + 16u <= B.un) {
                         uint4 x, y;
-                        if (m + k + 16u <= un) {
-                            __builtin_memcpy(&x, in + m + k, 16);
-                            __builtin_memcpy(&y, in + cm + k, 16);
-                        } else {
-                            uint32_t xb[4] = {0, 0, 0, 0}, yb[4] = {0, 0, 0, 0};
-                            for (uint32_t t = 0; t < 16u && m + k + t < un; t++) {
-                                xb[t >> 2] |= (uint32_t)in[m + k + t] << (8 * (t & 3));
-                                yb[t >> 2] |= (uint32_t)in[cm + k + t] << (8 * (t & 3));
+                        __builtin_memcpy(&x, B.in + m + kk, 16);
+                        __builtin_memcpy(&y, B.in + cm + kk, 16);
+                        xb[0] = x.x; xb[1] = x.y; xb[2] = x.z; xb[3] = x.w;
+                        yb[0] = y.x; yb[1] = y.y; yb[2] = y.z; yb[3] = y.w;
+                    } else {
+#pragma unroll
+                        for (uint32_t t = 0; t < 16u; t++) {
+                            if (m + kk + t < B.un) {
+                                xb[t >> 2] |= (uint32_t)B.in[m + kk + t] << (8 * (t & 3));
+                                yb[t >> 2] |= (uint32_t)B.in[cm + kk + t] << (8 * (t & 3));
                             }
-                            x = make_uint4(xb[0], xb[1], xb[2], xb[3]);
-                            y = make_uint4(yb[0], yb[1], yb[2], yb[3]);
                         }
-                        const uint32_t e0 = x.x ^ y.x, e1 = x.y ^ y.y, e2 = x.z ^ y.z, e3 = x.w ^ y.w;
-                        if (e0) { d = 1; at = __builtin_ctz(e0) >> 3; }
-                        else if (e1) { d = 1; at = 4 + (__builtin_ctz(e1) >> 3); }
-                        else if (e2) { d = 1; at = 8 + (__builtin_ctz(e2) >> 3); }
-                        else if (e3) { d = 1; at = 12 + (__builtin_ctz(e3) >> 3); }
                     }
-                    const uint64_t bad = __ballot(d != 0 || k >= lm);
-                    if (bad) {
-                        const int fl = __builtin_ctzll(bad);
-                        const uint32_t kk = L + 16u * (uint32_t)fl;
-                        L = kk >= lm ? lm : kk + lane_val(at, fl);
-                        break;
-                    }
-                    L += 1024u;
-                }
-                if (L > lm) L = lm;
-                STAT_ADD(12, 1);
-            }
-            uint32_t bkj = (v >> 16) & 7u;
-            if (bkj > m - anchor) bkj = m - anchor;   // never back into emitted bytes
-            if (lane == (int)j) { m_back = bkj; m_len = L + bkj; }
-            members |= 1ull << j;
-            q = m + L;
-            anchor = q;
-        }
-        STAT(1);
-
-        // ---- 3. table updates: walked positions, then match_end - 2 ----
-        if (((walked >> lane) & 1ull) && hashable) S.tab[h] = (uint16_t)p;
-        const bool mem = (members >> lane) & 1ull;
-        if (mem) {
-            const uint32_t e2 = p + (m_len - m_back) - 2u;   // match end - 2
-            if (e2 + 5u <= un) {
-                uint32_t lo32 = 0, b4 = 0;
-                if (e2 >= rlo && e2 + 8u <= fill) {
-                    lo32 = ring4(S, e2);
-                    b4 = ring4(S, e2 + 4u);
-                } else if (e2 + 8u <= un) {
-                    uint2 t;
-                    __builtin_memcpy(&t, in + e2, 8);
-                    lo32 = t.x;
-                    b4 = t.y;
-                } else {
-                    for (uint32_t t = 0; t < 5u; t++) {
-                        const uint32_t by = in[e2 + t];
-                        if (t < 4) lo32 |= by << (8 * t); else b4 = by;
+#pragma unroll
+                    for (int t = 3; t >= 0; t--) {
+                        const uint32_t e = xb[t] ^ yb[t];
+                        if (e) { d = 1; at = 4u * (uint32_t)t + (__builtin_ctz(e) >> 3); }
                     }
                 }
-                wave_sync();
-                S.tab[hash5(lo32, b4)] = (uint16_t)e2;
-            }
-        }
-        wave_sync();
-        STAT(2);
-
-        // ---- 4. emission ----
-        if (members) {
-            const uint32_t ms = p - m_back;              // match start after catch-up
-            const uint32_t end = ms + m_len;
-            const uint32_t an = umax(wave_shr1(wave_incl_max(mem ? end : 0u), 0u), anchor0);
-            const uint32_t lit = mem ? ms - an : 0u;
-            const uint32_t ml = m_len - kMinMatch;
-            const uint32_t hdr = 1u + ext_bytes(lit);
-            const uint32_t size = mem ? hdr + lit + 2u + ext_bytes(ml) : 0u;
-            const uint32_t ex = wave_excl_scan(size);
-            const uint32_t tot = lane_val(ex + size, 63);
-            if ((uint64_t)o + tot > cap) {
-                overflow = true;
-                break;
-            }
-            const uint32_t ol = o + ex;
-            if (mem) {
-                uint8_t *d = dst + ol;
-                d[0] = (uint8_t)(((lit < 15u ? lit : 15u) << 4) | (ml < 15u ? ml : 15u));
-                put_len(d + 1, lit);
-                if (lit <= kLongLit) {
-                    // exact-length copy: whole dwords, then the tail bytes
-                    uint32_t k = 0;
-                    const bool inring = an >= rlo;   // an + lit <= fill always
-                    for (; k + 4u <= lit; k += 4u) {
-                        uint32_t v;
-                        if (inring) v = ring4(S, an + k);
-                        else __builtin_memcpy(&v, in + an + k, 4);
-                        __builtin_memcpy(d + hdr + k, &v, 4);
-                    }
-                    if (k < lit) {
-                        uint32_t v;
-                        if (inring) v = ring4(S, an + k);
-                        else { v = 0; for (uint32_t t = 0; k + t < lit; t++) v |= (uint32_t)in[an + k + t] << (8 * t); }
-                        for (; k < lit; k++, v >>= 8) d[hdr + k] = (uint8_t)v;
-                    }
+                const uint64_t bad = __ballot(d != 0 || kk >= lm);
+                if (bad) {
+                    const int fl = __builtin_ctzll(bad);
+                    const uint32_t k2 = L + 16u * (uint32_t)fl;
+                    L = k2 >= lm ? lm : k2 + lane_val(at, fl);
+                    break;
                 }
-                const uint32_t off = p - c;
-                uint8_t *t = d + hdr + lit;
-                t[0] = (uint8_t)off;
-                t[1] = (uint8_t)(off >> 8);
-                put_len(t + 2, ml);
+                L += 1024u;
             }
-            // long literal runs: the whole wave copies them, one member at a time
-            uint64_t longm = __ballot(mem && lit > kLongLit);
-            while (longm) {
-                const int l = __builtin_ctzll(longm);
-                longm &= longm - 1ull;
-                const uint32_t la = lane_val(an, l), ll = lane_val(lit, l);
-                const uint32_t lo = lane_val(ol + hdr, l);
-                wave_copy(in, dst, la, lo, ll, lane);
-            }
-            o += tot;
-            STAT_ADD(11, __popcll(members));
+            if (L > lm) L = lm;
         }
-        if (refill) {
-            wave_sync();
-            chunk_store(S, fill, lane, pre);
-            fill += kChunkE;
-            rlo = umax(rlo, fill - kRingE);
-        }
-        STAT(3);
-        STAT_ADD(10, 1);
-        P = q;
+        uint32_t bkj = (v >> 8) & 7u;
+        if (bkj > m - C.anchor) bkj = m - C.anchor;   // never back into emitted bytes
+        if (lane == (int)j) { C.m_back = bkj; C.m_len = L + bkj; }
+        C.members |= 1ull << j;
+        q = m + L;
+        C.anchor = q;
     }
+    C.q = q;
+}
 
+// second half: table updates, then emission of chunk k's sequences
+__device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int lane, Cons &C) {
+    if (C.overflow) return;
+    const uint32_t P = 64u * (uint32_t)k;
+    const uint32_t p = P + (uint32_t)lane;
+    const uint2 iv = S.info[k & 1][lane];
+    if (((C.walked >> lane) & 1ull) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
+    const bool mem = (C.members >> lane) & 1ull;
+    // the ring holds input [rlo, P + 128) during this half
+    const uint32_t rlo = P + 128u > kRingE ? P + 128u - kRingE : 0u;
+    const uint32_t fwd = C.m_len - C.m_back;     // match length from p
+    // match_end - 2: hashed by the producer unless the consumer extended the match
+    uint32_t e2h = (iv.x >> 16) & (kHSize - 1);
+    bool e2ok = mem && (iv.x & I_E2) && !(iv.x & I_TRUNC);
+    if (mem && (iv.x & I_TRUNC)) {
+        const uint32_t e2 = p + fwd - 2u;
+        if (e2 + 5u <= B.un) {
+            uint32_t lo32 = 0, b4 = 0;
+            for (uint32_t t = 0; t < 5u; t++) {
+                const uint32_t by = B.in[e2 + t];
+                if (t < 4) lo32 |= by << (8 * t); else b4 = by;
+            }
+            e2h = hash5(lo32, b4);
+            e2ok = true;
+        }
+    }
+    wave_sync();
+    if (e2ok) S.tab[e2h] = (uint16_t)(p + fwd - 2u);
+    if (!C.members) return;
+    const uint32_t ms = p - C.m_back;            // match start after catch-up
+    const uint32_t end = ms + C.m_len;
+    const uint32_t an = umax(wave_shr1(wave_incl_max(mem ? end : 0u), 0u), C.anchor0);
+    const uint32_t lit = mem ? ms - an : 0u;
+    const uint32_t ml = C.m_len - kMinMatch;
+    const uint32_t hdr = 1u + ext_bytes(lit);
+    const uint32_t size = mem ? hdr + lit + 2u + ext_bytes(ml) : 0u;
+    const uint32_t ex = wave_excl_scan(size);
+    const uint32_t tot = lane_val(ex + size, 63);
+    if ((uint64_t)C.o + tot > B.cap) {
+        C.overflow = true;
+        return;
+    }
+    const uint32_t ol = C.o + ex;
+    if (mem) {
+        uint8_t *d = B.dst + ol;
+        d[0] = (uint8_t)(((lit < 15u ? lit : 15u) << 4) | (ml < 15u ? ml : 15u));
+        put_len(d + 1, lit);
+        if (lit <= kLongLit) {
+            const bool inring = an >= rlo;       // an + lit <= P + 64
+            uint32_t t = 0;
+            for (; t + 4u <= lit; t += 4u) {
+                uint32_t v;
+                if (inring) v = ring4(S, an + t);
+                else __builtin_memcpy(&v, B.in + an + t, 4);
+                __builtin_memcpy(d + hdr + t, &v, 4);
+            }
+            for (; t < lit; t++)
+                d[hdr + t] = inring ? (uint8_t)ring4(S, an + t) : B.in[an + t];
+        }
+        const uint32_t off = iv.y & 0xFFFFu;
+        uint8_t *tk = d + hdr + lit;
+        tk[0] = (uint8_t)off;
+        tk[1] = (uint8_t)(off >> 8);
+        put_len(tk + 2, ml);
+    }
+    uint64_t longm = __ballot(mem && lit > kLongLit);
+    while (longm) {
+        const int l = __builtin_ctzll(longm);
+        longm &= longm - 1ull;
+        wave_copy(B.in, B.dst, lane_val(an, l), lane_val(ol + hdr, l), lane_val(lit, l), lane);
+    }
+    C.o += tot;
+}
+
+template <bool SMALL>
+__device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, int lane,
+                                             int *result) {
+    STATS_DECL
+    Prod Pr;
+    Cons C;
+    C.q = 0;
+    C.anchor = 0;
+    C.o = 0;
+    C.overflow = false;
+    C.walked = C.members = 0;
+    C.m_back = C.m_len = C.anchor0 = 0;
+    const int nch = B.n >= kMinLength ? B.nch : 0;   // :584, shorter -> last literals only
+
+    if (wave == 1 && nch > 0) {  // prologue: A(0..2), B(0), B(1), C1(0)
+        uint32_t X0[8], Y0[8];
+        uint32_t cT0, jL0, h0;
+        prod_load<SMALL>(B, 0, lane, X0);
+        prod_load<SMALL>(B, 1, lane, Pr.X1);
+        prod_load<SMALL>(B, 2, lane, Pr.X2);
+        prod_lookup<SMALL>(S, B, 0, lane, X0, cT0, jL0, h0, Y0);
+        prod_lookup<SMALL>(S, B, 1, lane, Pr.X1, Pr.cT1, Pr.jL1, Pr.h1, Pr.Y1);
+        prod_measure<SMALL>(B, 0, lane, X0, Y0, cT0, jL0, h0, Pr.q0, Pr.E0);
+    }
+    __syncthreads();
+    for (int s = 0; s <= nch; s++) {
+        // ---- first half: producer A(s+3), B(s+2) | consumer walks chunk s-1 ----
+        if (wave == 1) {
+            if (s + 2 < nch) {
+                prod_load<SMALL>(B, s + 3, lane, Pr.X3);
+                prod_lookup<SMALL>(S, B, s + 2, lane, Pr.X2, Pr.cT2, Pr.jL2, Pr.h2, Pr.Y2);
+            }
+        } else if (s >= 1) {
+            cons_walk(S, B, s - 1, lane, C);
+            STAT(0);
+        }
+        __syncthreads();
+        STAT(4);
+        // ---- second half: producer C1(s+1), C2(s) | consumer table + emission of s-1 ----
+        if (wave == 1) {
+            if (s < nch) {
+                if (s + 1 < nch)
+                    prod_measure<SMALL>(B, s + 1, lane, Pr.X1, Pr.Y1, Pr.cT1, Pr.jL1, Pr.h1, Pr.q1,
+                                        Pr.E1);
+                prod_finish(S, B, s, lane, Pr.q0, Pr.E0);
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    Pr.X1[t] = Pr.X2[t];
+                    Pr.X2[t] = Pr.X3[t];
+                    Pr.Y1[t] = Pr.Y2[t];
+                    Pr.E0[t] = Pr.E1[t];
+                }
+                Pr.cT1 = Pr.cT2;
+                Pr.jL1 = Pr.jL2;
+                Pr.h1 = Pr.h2;
+                Pr.q0 = Pr.q1;
+            }
+        } else if (s >= 1) {
+            cons_emit(S, B, s - 1, lane, C);
+            STAT(1);
+            STAT_ADD(11, __popcll(C.members));
+        }
+        STAT_ADD(10, 1);
+        __syncthreads();
+        STAT(3);
+    }
+    if (wave != 0) return;
     // ---- last literals (:732-751) ----
-    if (!overflow) {
-        const uint32_t lit = un - anchor;
+    if (!C.overflow) {
+        const uint32_t lit = B.un - C.anchor;
         const uint32_t hdr = 1u + ext_bytes(lit);
-        const uint32_t total = o + hdr + lit;
-        if (total > cap) {
-            overflow = true;
+        const uint32_t total = C.o + hdr + lit;
+        if (total > B.cap) {
+            C.overflow = true;
         } else {
             if (lane == 0) {
-                dst[o] = (uint8_t)((lit < 15u ? lit : 15u) << 4);
-                put_len(dst + o + 1, lit);
+                B.dst[C.o] = (uint8_t)((lit < 15u ? lit : 15u) << 4);
+                put_len(B.dst + C.o + 1, lit);
             }
-            wave_copy(in, dst, anchor, o + hdr, lit, lane);
-            o = total;
+            wave_copy(B.in, B.dst, C.anchor, C.o + hdr, lit, lane);
+            C.o = total;
         }
     }
-    if (lane == 0) a.result[b] = overflow ? 0 : (int)o;
-    STAT(4);
+    if (lane == 0) *result = C.overflow ? 0 : (int)C.o;
+    STAT(2);
     STAT_ADD(13, 1);
     STATS_FLUSH(g_enc_stats);
 }
 
+}  // namespace
+
+__global__ void __launch_bounds__(128)
+lz4_encode_kernel(BlockArgs a) {
+    __shared__ EncLds S;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+
+    Blk B;
+    B.in = (const uint8_t *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
+    B.dst = (uint8_t *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
+    B.n = a.src_size[b];
+    const int icap = a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride;
+    if (B.n < 0 || B.n > kMaxBlock || icap < 0) {
+        if (tid == 0) a.result[b] = (B.n > kMaxBlock) ? kErange : 0;
+        return;
+    }
+    B.cap = (uint32_t)icap;
+    B.un = (uint32_t)B.n;
+    B.mstart = B.un >= 12 ? B.un - 12 : 0;   // matches start at <= n-12 (:585)
+    B.mlimit = B.un >= 5 ? B.un - 5 : 0;     // and end at <= n-5 (:633)
+    B.nch = (B.n + 63) / 64;
+
+    // table = 0 (the reference's memset state: position 0 for every hash)
+    for (int i = tid; i < kHSize / 8; i += 128) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < 256; i += 128) S.scr[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    if (B.n < kSmall) encode_block<true>(S, B, wave, lane, &a.result[b]);
+    else encode_block<false>(S, B, wave, lane, &a.result[b]);
+}
+
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(lz4_encode_kernel, dim3(a.nblocks), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(lz4_encode_kernel, dim3(a.nblocks), dim3(128), 0, s, a);
     return hipGetLastError();
 }
 

@@ -15,8 +15,8 @@ sys.path.insert(0, ROOT)
 
 DEC = ["parse", "copy", "(batches)", "(steps)", "(restages)", "", "", "", "", "", "(blocks)", "", "", "",
        "", ""]
-ENC = ["candidates", "walk", "table", "emit", "last", "", "", "", "", "", "(rounds)",
-       "(members)", "(extensions)", "(blocks)", "", ""]
+ENC = ["walk", "table+emit", "last", "wait end-barrier", "wait mid-barrier", "", "", "", "", "",
+       "(steps)", "(members)", "", "(blocks)", "", ""]
 
 
 def main():
