@@ -67,16 +67,16 @@ __device__ __forceinline__ void wave_sync() {
 // Aligned dword of the compressed block at byte offset `off` (src + off is
 // 4-aligned); bytes outside [0, csize) read as 0 and nothing beyond that dword
 // (which cannot cross a page) is touched.
-__device__ __forceinline__ uint32_t src_dword(const uint8_t *src, int csize, int off) {
+__device__ __forceinline__ uint32_t src_dword(gcu8 *src, int csize, int off) {
     if (off >= csize || off <= -4) return 0u;
-    uint32_t v = *(const uint32_t *)(src + off);
+    uint32_t v = *(__attribute__((address_space(1))) const uint32_t *)(src + off);
     if (off < 0) v &= 0xFFFFFFFFu << (8 * (-off));
     if (off + 4 > csize) v &= 0xFFFFFFFFu >> (8 * (off + 4 - csize));
     return v;
 }
 
 // Stage src[s0 .. s0 + kStage) into LDS (src + s0 4-aligned; zero outside the input).
-__device__ __forceinline__ void stage_load(WaveLds &L, const uint8_t *src, int csize, int s0,
+__device__ __forceinline__ void stage_load(WaveLds &L, gcu8 *src, int csize, int s0,
                                            int lane) {
     uint32_t v[kStage / 256];
 #pragma unroll
@@ -86,26 +86,20 @@ __device__ __forceinline__ void stage_load(WaveLds &L, const uint8_t *src, int c
 }
 
 // 4-aligned staging start at or below p
-__device__ __forceinline__ int stage_base(const uint8_t *src, int p) {
+__device__ __forceinline__ int stage_base(gcu8 *src, int p) {
     return p - (int)((uintptr_t)(src + p) & 3u);
 }
 
 // byte p of the compressed block for the scalar path (wave-uniform p)
-__device__ __forceinline__ uint32_t sbyte(const WaveLds &L, const uint8_t *src, int csize, int s0,
+__device__ __forceinline__ uint32_t sbyte(const WaveLds &L, gcu8 *src, int csize, int s0,
                                           int p) {
     const uint32_t r = (uint32_t)(p - s0);
     if (r < (uint32_t)kStage) return L.stage[r];
-    return p < csize ? (uint32_t)src[p] : 0u;
+    return p < csize ? (uint32_t)src[(uint32_t)p] : 0u;
 }
 
-// 4 bytes at src[a] (a + 3 < csize): one or two aligned dword loads
-__device__ __forceinline__ uint32_t src4(const uint8_t *src, uint32_t a) {
-    const uint8_t *p = src + a;
-    const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
-    const uint32_t *w = (const uint32_t *)(p - sh);
-    const uint32_t lo = w[0];
-    return sh ? funnel(w[1], lo, sh) : lo;
-}
+// 4 bytes at src[a] (a + 3 < csize)
+__device__ __forceinline__ uint32_t src4(gcu8 *src, uint32_t a) { return gload4(src + a); }
 
 }  // namespace
 
@@ -124,8 +118,8 @@ hipError_t dec_stats_read(unsigned long long *out, int reset) {
 namespace {
 
 struct Dec {
-    const uint8_t *src;
-    uint8_t *dst;
+    gcu8 *src;
+    gu8 *dst;
     int csize, cap;
     int64_t oexit;
     int s0;          // staged window start
@@ -393,9 +387,11 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
             if (kind[j] == 1) v = lds[addr[j]];
             else if (kind[j] == 2) {
                 if (isdst[j]) {
-                    const uint8_t *pp = D.dst + addr[j];
+                    gcu8 *pp = D.dst + addr[j];
                     const uint32_t sh = (uint32_t)((uintptr_t)pp & 3u);
-                    v = (__builtin_nontemporal_load((const uint32_t *)(pp - sh)) >> (8 * sh)) & 0xFFu;
+                    v = (__builtin_nontemporal_load(
+                             (__attribute__((address_space(1))) const uint32_t *)(pp - sh)) >>
+                         (8 * sh)) & 0xFFu;
                 } else {
                     v = D.src[addr[j]];
                 }
@@ -405,11 +401,11 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
     }
     wave_sync();
     // store: ring and dst
-    uint8_t *o8 = D.dst + q0;
+    gu8 *o8 = D.dst + q0;
     if (q0 >= lo && q0 + 4u <= hi) {
         *(uint32_t *)&L.ring[q0 & (kRing - 1)] = word;
         if ((((uintptr_t)o8) & 3u) == 0) {
-            *(uint32_t *)o8 = word;
+            *(__attribute__((address_space(1))) uint32_t *)o8 = word;
         } else {
 #pragma unroll
             for (int j = 0; j < 4; j++) o8[j] = (uint8_t)(word >> (8 * j));
@@ -436,8 +432,8 @@ lz4_decode_kernel(BlockArgs a) {
     const int lane = threadIdx.x;
 
     Dec D;
-    D.src = (const uint8_t *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
-    D.dst = (uint8_t *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
+    D.src = (gcu8 *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
+    D.dst = (gu8 *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
     D.csize = a.src_size[b];
     D.cap = a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride;
     D.oexit = PARTIAL ? a.target[b] : 0;

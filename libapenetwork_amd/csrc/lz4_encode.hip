@@ -59,8 +59,7 @@ namespace {
 constexpr int kHLog = APE_LZ4_HLOG;
 constexpr int kHSize = 1 << kHLog;
 constexpr uint32_t kEagerLen = 28;   // match bytes measured by the producer
-constexpr uint32_t kLongLit = 32;    // longer literal runs are copied by the wave
-constexpr uint32_t kRingE = 4096;    // recent input bytes for the consumer
+constexpr uint32_t kRingE = 2048;    // recent input bytes (literals, stage 2, end-2)
 constexpr int kSmall = 128;          // smaller blocks take the byte-load path
 
 constexpr uint32_t kEager2 = kEagerLen + 32;  // after the producer's second stage
@@ -75,6 +74,8 @@ struct __attribute__((aligned(16))) EncLds {
     uint32_t ring[kRingE / 4];       // input byte x at ring byte (x mod kRingE)
     uint2 info[2][64];
     uint32_t scr[256];               // producer scratch: earliest lane per low hash bits
+    uint4 rec[64];                   // consumer: sequence records of the chunk being emitted
+    uint32_t omap[16];               // consumer: owner map of a 64-byte output window
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -116,21 +117,19 @@ __device__ __forceinline__ void shift_bytes(const uint32_t (&L)[8], int d, uint3
 // clamped window, fixed up with ALU only (so the wave's vmcnt accounting stays
 // static in the pipelined loop).
 template <bool SMALL>
-__device__ __forceinline__ void load32(const uint8_t *in, int n, int pos, uint32_t (&X)[8]) {
+__device__ __forceinline__ void load32(gcu8 *in, int n, int pos, uint32_t (&X)[8]) {
     if (SMALL) {
 #pragma unroll
         for (int k = 0; k < 8; k++) X[k] = 0;
 #pragma unroll
         for (int k = 0; k < 32; k++) {
             const int q = pos + k;
-            if (q >= 0 && q < n) X[k >> 2] |= (uint32_t)in[q] << (8 * (k & 3));
+            if (q >= 0 && q < n) X[k >> 2] |= (uint32_t)in[(uint32_t)q] << (8 * (k & 3));
         }
         return;
     }
     const int ca = pos < 0 ? 0 : (pos > n - 32 ? n - 32 : pos);
-    uint4 a, b;
-    __builtin_memcpy(&a, in + ca, 16);
-    __builtin_memcpy(&b, in + ca + 16, 16);
+    const uint4 a = gload16(in + (uint32_t)ca), b = gload16(in + ((uint32_t)ca + 16u));
     const uint32_t L[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     if (ca == pos) {
 #pragma unroll
@@ -175,7 +174,7 @@ __device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {  // bytes after a 15
 }
 
 // write the length extension of v (>= 15) at o
-__device__ __forceinline__ void put_len(uint8_t *o, uint32_t v) {
+__device__ __forceinline__ void put_len(gu8 *o, uint32_t v) {
     if (v < 15) return;
     v -= 15;
     uint32_t k = 0;
@@ -201,13 +200,11 @@ __device__ __forceinline__ void ring32(const EncLds &S, uint32_t x, uint32_t (&O
 }
 
 // Copy in[a, a+len) to dst[o, o+len) with the whole wave (16 bytes per lane per step).
-__device__ __forceinline__ void wave_copy(const uint8_t *in, uint8_t *dst, uint32_t a, uint32_t o,
+__device__ __forceinline__ void wave_copy(gcu8 *in, gu8 *dst, uint32_t a, uint32_t o,
                                           uint32_t len, int lane) {
     for (uint32_t k = 16u * (uint32_t)lane; k < len; k += 1024u) {
         if (k + 16u <= len) {
-            uint4 v;
-            __builtin_memcpy(&v, in + a + k, 16);
-            __builtin_memcpy(dst + o + k, &v, 16);
+            gstore16(dst + (o + k), gload16(in + (a + k)));
         } else {
             for (uint32_t t = k; t < len; t++) dst[o + t] = in[a + t];
         }
@@ -215,8 +212,8 @@ __device__ __forceinline__ void wave_copy(const uint8_t *in, uint8_t *dst, uint3
 }
 
 struct Blk {
-    const uint8_t *in;
-    uint8_t *dst;
+    gcu8 *in;
+    gu8 *dst;
     int n;
     uint32_t un, cap, mstart, mlimit;
     int nch;                         // chunks of 64 positions
@@ -299,7 +296,11 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     uint32_t len = R.len;
     bool trunc = false;
+#ifdef APE_EXP_NO_STAGE2
+    if (false) {
+#else
     if (R.trunc1) {
+#endif
         uint32_t O[8];
         ring32(S, p + kEagerLen, O);             // own bytes p+28 .. p+60
         uint32_t ext = 32;
@@ -338,6 +339,9 @@ __device__ __forceinline__ void cons_walk(const EncLds &S, const Blk &B, int k, 
     C.walked = 0;
     C.members = 0;
     C.anchor0 = C.anchor;
+#ifdef APE_EXP_NO_WALK
+    return;
+#endif
     if (C.overflow || C.q >= P + 64u) return;
     const uint2 iv = S.info[k & 1][lane];
     const uint64_t Mm = __ballot((iv.x & I_HAS) != 0u);
@@ -366,9 +370,7 @@ __device__ __forceinline__ void cons_walk(const EncLds &S, const Blk &B, int k, 
                 if (kk < lm) {
                     uint32_t xb[4] = {0, 0, 0, 0}, yb[4] = {0, 0, 0, 0};
                     if (m + kk + 16u <= B.un) {
-                        uint4 x, y;
-                        __builtin_memcpy(&x, B.in + m + kk, 16);
-                        __builtin_memcpy(&y, B.in + cm + kk, 16);
+                        const uint4 x = gload16(B.in + (m + kk)), y = gload16(B.in + (cm + kk));
                         xb[0] = x.x; xb[1] = x.y; xb[2] = x.z; xb[3] = x.w;
                         yb[0] = y.x; yb[1] = y.y; yb[2] = y.z; yb[3] = y.w;
                     } else {
@@ -415,8 +417,9 @@ __device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int la
     const uint2 iv = S.info[k & 1][lane];
     if (((C.walked >> lane) & 1ull) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
     const bool mem = (C.members >> lane) & 1ull;
-    // the ring holds input [rlo, P + 128) during this half
-    const uint32_t rlo = P + 128u > kRingE ? P + 128u - kRingE : 0u;
+    // during this half the producer has written chunks up to k + 3, so the ring
+    // holds input [rlo, P + 256)
+    const uint32_t rlo = P + 256u > kRingE ? P + 256u - kRingE : 0u;
     const uint32_t fwd = C.m_len - C.m_back;     // match length from p
     // match_end - 2: hashed by the producer unless the consumer extended the match
     uint32_t e2h = (iv.x >> 16) & (kHSize - 1);
@@ -435,48 +438,62 @@ __device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int la
     }
     wave_sync();
     if (e2ok) S.tab[e2h] = (uint16_t)(p + fwd - 2u);
+#ifdef APE_EXP_NO_EMIT
+    C.members = 0;
+#endif
     if (!C.members) return;
     const uint32_t ms = p - C.m_back;            // match start after catch-up
     const uint32_t end = ms + C.m_len;
     const uint32_t an = umax(wave_shr1(wave_incl_max(mem ? end : 0u), 0u), C.anchor0);
     const uint32_t lit = mem ? ms - an : 0u;
     const uint32_t ml = C.m_len - kMinMatch;
-    const uint32_t hdr = 1u + ext_bytes(lit);
-    const uint32_t size = mem ? hdr + lit + 2u + ext_bytes(ml) : 0u;
+    const uint32_t size = mem ? 1u + ext_bytes(lit) + lit + 2u + ext_bytes(ml) : 0u;
     const uint32_t ex = wave_excl_scan(size);
     const uint32_t tot = lane_val(ex + size, 63);
     if ((uint64_t)C.o + tot > B.cap) {
         C.overflow = true;
         return;
     }
-    const uint32_t ol = C.o + ex;
-    if (mem) {
-        uint8_t *d = B.dst + ol;
-        d[0] = (uint8_t)(((lit < 15u ? lit : 15u) << 4) | (ml < 15u ? ml : 15u));
-        put_len(d + 1, lit);
-        if (lit <= kLongLit) {
-            const bool inring = an >= rlo;       // an + lit <= P + 64
-            uint32_t t = 0;
-            for (; t + 4u <= lit; t += 4u) {
-                uint32_t v;
-                if (inring) v = ring4(S, an + t);
-                else __builtin_memcpy(&v, B.in + an + t, 4);
-                __builtin_memcpy(d + hdr + t, &v, 4);
+    // Gather: lane L of window w produces output byte w + L.  Its sequence is the
+    // last member starting at or before it (owner map + prefix max).
+    if (mem) S.rec[lane] = make_uint4(ex, an, lit, ml | ((iv.y & 0xFFFFu) << 16));
+    gu8 *out = B.dst + C.o;
+    for (uint32_t w = 0; w < tot; w += 64u) {
+        if (lane < 16) S.omap[lane] = 0u;
+        wave_sync();
+        if (mem && ex > w && ex < w + 64u) ((uint8_t *)S.omap)[ex - w] = (uint8_t)(lane + 1);
+        wave_sync();
+        const uint32_t mk = ((const uint8_t *)S.omap)[lane];
+        const uint64_t cov = __ballot(mem && ex <= w);   // member 0 starts at 0
+        const uint32_t carry = 64u - (uint32_t)__clzll((long long)cov);
+        const uint32_t own = umax(wave_incl_max(mk), carry) - 1u;
+        const uint4 r = S.rec[own];
+        const uint32_t b = w + (uint32_t)lane;
+        if (b < tot) {
+            const uint32_t rr = b - r.x;                 // offset inside the sequence
+            const uint32_t rl = r.z, rml = r.w & 0xFFFFu, roff = r.w >> 16;
+            const uint32_t lit_at = 1u + ext_bytes(rl), off_at = lit_at + rl;
+            uint32_t v;
+            if (rr == 0u) {
+                v = ((rl < 15u ? rl : 15u) << 4) | (rml < 15u ? rml : 15u);
+            } else if (rr < lit_at) {                    // literal-length extension
+                const uint32_t e = rl - 15u, full = e / 255u;
+                v = (rr - 1u < full) ? 255u : e - 255u * full;
+            } else if (rr < off_at) {                    // literal byte
+                const uint32_t a = r.y + (rr - lit_at);
+                v = a >= rlo ? (uint32_t)((const uint8_t *)S.ring)[a & (kRingE - 1)]
+                             : (uint32_t)B.in[a];
+            } else if (rr == off_at) {
+                v = roff & 0xFFu;
+            } else if (rr == off_at + 1u) {
+                v = roff >> 8;
+            } else {                                     // match-length extension
+                const uint32_t e = rml - 15u, full = e / 255u;
+                v = (rr - off_at - 2u < full) ? 255u : e - 255u * full;
             }
-            for (; t < lit; t++)
-                d[hdr + t] = inring ? (uint8_t)ring4(S, an + t) : B.in[an + t];
+            out[b] = (uint8_t)v;
         }
-        const uint32_t off = iv.y & 0xFFFFu;
-        uint8_t *tk = d + hdr + lit;
-        tk[0] = (uint8_t)off;
-        tk[1] = (uint8_t)(off >> 8);
-        put_len(tk + 2, ml);
-    }
-    uint64_t longm = __ballot(mem && lit > kLongLit);
-    while (longm) {
-        const int l = __builtin_ctzll(longm);
-        longm &= longm - 1ull;
-        wave_copy(B.in, B.dst, lane_val(an, l), lane_val(ol + hdr, l), lane_val(lit, l), lane);
+        wave_sync();
     }
     C.o += tot;
 }
@@ -513,12 +530,13 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
                 prod_load<SMALL>(B, s + 3, lane, Pr.X3);
                 prod_lookup<SMALL>(S, B, s + 2, lane, Pr.X2, Pr.cT2, Pr.jL2, Pr.h2, Pr.Y2);
             }
+            STAT(5);
         } else if (s >= 1) {
             cons_walk(S, B, s - 1, lane, C);
             STAT(0);
         }
         __syncthreads();
-        STAT(4);
+        if (wave == 1) STAT(6); else STAT(4);
         // ---- second half: producer C1(s+1), C2(s) | consumer table + emission of s-1 ----
         if (wave == 1) {
             if (s < nch) {
@@ -538,6 +556,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
                 Pr.h1 = Pr.h2;
                 Pr.q0 = Pr.q1;
             }
+            STAT(7);
         } else if (s >= 1) {
             cons_emit(S, B, s - 1, lane, C);
             STAT(1);
@@ -545,9 +564,12 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         }
         STAT_ADD(10, 1);
         __syncthreads();
-        STAT(3);
+        if (wave == 1) STAT(8); else STAT(3);
     }
-    if (wave != 0) return;
+    if (wave != 0) {
+        STATS_FLUSH_TID(g_enc_stats, 64);
+        return;
+    }
     // ---- last literals (:732-751) ----
     if (!C.overflow) {
         const uint32_t lit = B.un - C.anchor;
@@ -572,7 +594,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
 
 }  // namespace
 
-__global__ void __launch_bounds__(128)
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
 lz4_encode_kernel(BlockArgs a) {
     __shared__ EncLds S;
     const int b = blockIdx.x;
@@ -580,8 +602,8 @@ lz4_encode_kernel(BlockArgs a) {
     const int lane = tid & 63, wave = tid >> 6;
 
     Blk B;
-    B.in = (const uint8_t *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
-    B.dst = (uint8_t *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
+    B.in = (gcu8 *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
+    B.dst = (gu8 *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
     B.n = a.src_size[b];
     const int icap = a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride;
     if (B.n < 0 || B.n > kMaxBlock || icap < 0) {

@@ -14,6 +14,35 @@ constexpr int kMinLength = 13;
 constexpr int kMaxBlock = 65536;  // GPU block limit (LZ4 window, benchmark block)
 constexpr int kErange = -2147483647 - 1;
 
+// Global-address-space byte pointers: global_load/store with an SGPR base and a
+// 32-bit offset instead of flat accesses (which also tie up lgkmcnt).
+typedef __attribute__((address_space(1))) const uint8_t gcu8;
+typedef __attribute__((address_space(1))) uint8_t gu8;
+typedef uint32_t u32x4_u __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32x2_u __attribute__((ext_vector_type(2), aligned(1)));
+typedef uint32_t u32_u __attribute__((aligned(1)));
+
+// unaligned 16 / 8 / 4-byte global accesses (the hardware handles any alignment)
+__device__ __forceinline__ uint4 gload16(gcu8 *p) {
+    const u32x4_u v = *(__attribute__((address_space(1))) const u32x4_u *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 gload8(gcu8 *p) {
+    const u32x2_u v = *(__attribute__((address_space(1))) const u32x2_u *)p;
+    return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ uint32_t gload4(gcu8 *p) {
+    return *(__attribute__((address_space(1))) const u32_u *)p;
+}
+__device__ __forceinline__ void gstore16(gu8 *p, uint4 v) {
+    u32x4_u w;
+    w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+    *(__attribute__((address_space(1))) u32x4_u *)p = w;
+}
+__device__ __forceinline__ void gstore4(gu8 *p, uint32_t v) {
+    *(__attribute__((address_space(1))) u32_u *)p = v;
+}
+
 // ---- wave64 helpers ----
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
@@ -72,12 +101,14 @@ __device__ __forceinline__ uint32_t lane_val(uint32_t v, int l) {  // l wave-uni
 #define STATS_DECL uint64_t st_t_ = clock64(); uint64_t st_acc_[16] = {0};
 #define STAT(i) do { uint64_t t_ = clock64(); st_acc_[i] += t_ - st_t_; st_t_ = t_; } while (0)
 #define STAT_ADD(i, v) (st_acc_[i] += (uint64_t)(v))
-#define STATS_FLUSH(arr) do { if (threadIdx.x == 0) { _Pragma("unroll") for (int i_ = 0; i_ < 16; i_++) atomicAdd(&(arr)[i_], (unsigned long long)st_acc_[i_]); } } while (0)
+#define STATS_FLUSH(arr) STATS_FLUSH_TID(arr, 0)
+#define STATS_FLUSH_TID(arr, t) do { if (threadIdx.x == (t)) { _Pragma("unroll") for (int i_ = 0; i_ < 16; i_++) if (st_acc_[i_]) atomicAdd(&(arr)[i_], (unsigned long long)st_acc_[i_]); } } while (0)
 #else
 #define STATS_DECL
 #define STAT(i) do {} while (0)
 #define STAT_ADD(i, v) do {} while (0)
 #define STATS_FLUSH(arr) do {} while (0)
+#define STATS_FLUSH_TID(arr, t) do {} while (0)
 #endif
 hipError_t stats_read(int which, unsigned long long *out, int reset);
 

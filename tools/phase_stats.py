@@ -15,8 +15,9 @@ sys.path.insert(0, ROOT)
 
 DEC = ["parse", "copy", "(batches)", "(steps)", "(restages)", "", "", "", "", "", "(blocks)", "", "", "",
        "", ""]
-ENC = ["walk", "table+emit", "last", "wait end-barrier", "wait mid-barrier", "", "", "", "", "",
-       "(steps)", "(members)", "", "(blocks)", "", ""]
+ENC = ["C walk", "C table+emit", "C last", "C wait end", "C wait mid", "P load+lookup",
+       "P wait mid", "P measure+finish", "P wait end", "", "(steps x2 waves)", "(members)", "",
+       "(blocks)", "", ""]
 
 
 def main():
