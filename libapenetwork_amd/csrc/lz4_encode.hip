@@ -599,7 +599,9 @@ lz4_encode_kernel(BlockArgs a) {
     __shared__ EncLds S;
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+    // readfirstlane: the wave index is wave-uniform, and the compiler must know it,
+    // or every value merged after the producer/consumer branches becomes a VGPR
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     Blk B;
     B.in = (gcu8 *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
