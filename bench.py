@@ -105,6 +105,7 @@ def main():
     import torch
 
     import libapenetwork_amd as amd
+    from libapenetwork_amd.sharding import reduce_max, reduce_sum, shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -133,7 +134,7 @@ def main():
 
     t0 = time.time()
     chunk = 1 << 16
-    first = rank * nb
+    first, _ = shard(rank, world, nb)
     for b0 in range(0, nb, chunk):
         amd.synth_blocks(src[b0:b0 + chunk], n, first + b0, kind)
         torch.cuda.synchronize()
@@ -167,10 +168,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = reduce_max(dist, elapsed, "cuda")
 
     # ---- correctness + ratio (outside the timed region) ----
     ok = bool((dres == n).all().item())
@@ -194,10 +192,8 @@ def main():
                 sample_ok &= (r == n and ob.raw[:n] == sb[j].tobytes())
         except OSError:
             sample_ok = None
-    if dist:
-        agg = torch.tensor([comp_bytes, int(ok)], dtype=torch.int64, device="cuda")
-        dist.all_reduce(agg, op=dist.ReduceOp.SUM)
-        comp_bytes, ok = int(agg[0].item()), int(agg[1].item()) == world
+    comp_bytes, nok = reduce_sum(dist, [comp_bytes, int(ok)], "cuda")
+    ok = nok == world
 
     total_bytes = nb * n * world
     ms_step = elapsed / args.steps * 1e3
