@@ -34,7 +34,10 @@ namespace apelz4 {
 
 namespace {
 
-constexpr int kRing = 8192;      // per-wave history ring (bytes, power of two)
+#ifndef APE_LZ4_DRING
+#define APE_LZ4_DRING 1024
+#endif
+constexpr int kRing = APE_LZ4_DRING;  // per-wave history ring (bytes, power of two)
 constexpr int kStage = 2304;     // staged compressed bytes per batch (9 dwords/lane)
 constexpr int kWinNeed = 84;     // a parse window reads up to P + 63 + 21
 constexpr int kStep = 256;       // output bytes per copy step (4 per lane)
@@ -98,8 +101,6 @@ __device__ __forceinline__ uint32_t sbyte(const WaveLds &L, gcu8 *src, int csize
     return p < csize ? (uint32_t)src[(uint32_t)p] : 0u;
 }
 
-// 4 bytes at src[a] (a + 3 < csize)
-__device__ __forceinline__ uint32_t src4(gcu8 *src, uint32_t a) { return gload4(src + a); }
 
 }  // namespace
 
@@ -272,7 +273,16 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     return st;
 }
 
+// x mod off for x < off + 3 (three conditional subtractions cover off = 1)
+__device__ __forceinline__ uint32_t reduce3(uint32_t x, uint32_t off) {
+    x = x >= off ? x - off : x;
+    x = x >= off ? x - off : x;
+    return x >= off ? x - off : x;
+}
+
 // Produce output [lo, hi) of the step at `base` from the batch's descriptors.
+// Branch-light: every byte gets an LDS address and (rarely) an HBM pointer; loads
+// are guarded by wave-uniform tests only, so the wave does not juggle exec masks.
 __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t base, uint32_t lo,
                                           uint32_t hi, uint32_t gdone, int nd, uint32_t d_out) {
     const int lane = D.lane;
@@ -291,44 +301,45 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
     const uint4 dB = L.desc[hasB ? A + 1u : A];
     const uint32_t outB = hasB ? dB.y : 0xFFFFFFFFu;
     const uint32_t leA = dA.y + dA.z, leB = dB.y + dB.z;
+    const uint32_t xlA = dA.x - dA.y, xlB = dB.x - dB.y;   // literal source - output
+    const uint32_t offA = dA.w, offB = dB.w;
     const uint32_t s0 = (uint32_t)D.s0;
-
     const uint32_t q0 = base + 4u * (uint32_t)lane;
-    // per byte: 0 = none, 1 = LDS (stage or ring), 2 = HBM (src literal / dst history), 3 = pending
-    uint32_t kind[4], addr[4];
-    bool isdst[4];
+
+    // offset of byte 0 inside A's match period (one division, only if some lane needs it)
+    uint32_t rA = q0 - leA;                       // valid when q0 >= leA
+    const bool needmod = q0 >= leA && offA != 0u && rA >= offA;
+    if (__any(needmod)) {
+        if (needmod) rA %= offA;
+    }
+
+    // per byte: source position, LDS address (0xFFFFFFFF = none), HBM kind (1 src, 2 dst)
+    uint32_t pos[4], lad[4], gk[4];
     uint32_t pendm = 0;
+    bool anyg = false;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const uint32_t q = q0 + j;
         const bool inB = q >= outB;
-        const uint32_t le = inB ? leB : leA;
-        const uint32_t dout = inB ? dB.y : dA.y;
-        const uint32_t dsrc = inB ? dB.x : dA.x;
-        const uint32_t off = inB ? dB.w : dA.w;
-        kind[j] = 0;
-        addr[j] = 0;
-        isdst[j] = false;
-        if (q >= lo && q < hi) {
-            if (q < le) {
-                const uint32_t a = dsrc + (q - dout);
-                const bool st = a - s0 < (uint32_t)kStage;
-                kind[j] = st ? 1u : 2u;
-                addr[j] = st ? a - s0 + (uint32_t)offsetof(WaveLds, stage) : a;
-            } else if (off != 0) {
-                uint32_t k = q - le;
-                if (k >= off) k %= off;  // overlapping match: period `off` from the match start
-                const uint32_t s = le - off + k;
-                if (s < gdone) { kind[j] = 2; addr[j] = s; isdst[j] = true; }
-                else if (s < lo) { kind[j] = 1; addr[j] = s & (kRing - 1); }
-                else { kind[j] = 3; addr[j] = s; pendm |= 1u << j; }
-            }
-            // offset 0: the reference copies stale dst bytes -> 0 here
-        }
+        const uint32_t le = inB ? leB : leA, off = inB ? offB : offA;
+        const bool lit = q < le;
+        const uint32_t mb = inB ? q - leB : (q0 >= leA ? rA + j : q - leA);
+        const uint32_t mpos = le - off + reduce3(mb, off);
+        const uint32_t ps = lit ? q + (inB ? xlB : xlA) : mpos;
+        const bool live = q >= lo && q < hi && (lit || off != 0u);  // offset 0 -> 0 (App. B)
+        const bool inst = ps - s0 < (uint32_t)kStage;
+        const bool ring = !lit && ps >= gdone && ps < lo;
+        const bool pend = live && !lit && ps >= lo;
+        pos[j] = ps;
+        lad[j] = !live ? 0xFFFFFFFFu
+                       : (lit ? (inst ? ps - s0 + (uint32_t)offsetof(WaveLds, stage) : 0xFFFFFFFFu)
+                              : (ring ? (ps & (kRing - 1)) : 0xFFFFFFFFu));
+        gk[j] = !live || pend ? 0u : (lit ? (inst ? 0u : 1u) : (ps < gdone ? 2u : 0u));
+        anyg |= gk[j] != 0u;
+        pendm |= pend ? 1u << j : 0u;
     }
-    // in-step sources: follow them through the owner map (short chains)
+    // in-step sources: follow them through the owner map (short chains, rare)
     if (__any(pendm != 0)) {
-        // owners of every byte of the step
         uint32_t ow = 0, pr = pre;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -341,70 +352,62 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
         while (__any(pendm != 0)) {
             if (pendm) {
                 const int j0 = __builtin_ctz(pendm);
-                uint32_t x = addr[0];
+                uint32_t x = pos[0];
 #pragma unroll
                 for (int j = 1; j < 4; j++)
-                    if (j == j0) x = addr[j];
+                    if (j == j0) x = pos[j];
                 const uint4 d = L.desc[((const uint8_t *)L.own)[x - base] - 1u];
                 const uint32_t le = d.y + d.z;
-                uint32_t nk, na;
-                bool nd2 = false;
+                uint32_t na, nl = 0xFFFFFFFFu, ng = 0;
+                bool still = false;
                 if (x < le) {
-                    const uint32_t a = d.x + (x - d.y);
-                    const bool st = a - s0 < (uint32_t)kStage;
-                    nk = st ? 1u : 2u;
-                    na = st ? a - s0 + (uint32_t)offsetof(WaveLds, stage) : a;
+                    na = d.x + (x - d.y);
+                    if (na - s0 < (uint32_t)kStage) nl = na - s0 + (uint32_t)offsetof(WaveLds, stage);
+                    else ng = 1;
                 } else if (d.w == 0) {
-                    nk = 0;
                     na = 0;
                 } else {
                     uint32_t k = x - le;
                     if (k >= d.w) k %= d.w;
-                    const uint32_t s = le - d.w + k;
-                    if (s < gdone) { nk = 2; na = s; nd2 = true; }
-                    else if (s < lo) { nk = 1; na = s & (kRing - 1); }
-                    else { nk = 3; na = s; }
+                    na = le - d.w + k;
+                    if (na < gdone) ng = 2;
+                    else if (na < lo) nl = na & (kRing - 1);
+                    else still = true;
                 }
 #pragma unroll
                 for (int j = 0; j < 4; j++)
-                    if (j == j0) { kind[j] = nk; addr[j] = na; isdst[j] = nd2; }
-                if (nk != 3) pendm &= pendm - 1u;
+                    if (j == j0) { pos[j] = na; lad[j] = nl; gk[j] = ng; }
+                anyg |= ng != 0u;
+                if (!still) pendm &= pendm - 1u;
             }
         }
     }
-    // fetch
-    uint32_t word = 0;
-    const bool lit4 = kind[0] == 2 && !isdst[0] && kind[1] == 2 && !isdst[1] && kind[2] == 2 &&
-                      !isdst[2] && kind[3] == 2 && !isdst[3] && addr[3] == addr[0] + 3u &&
-                      addr[1] == addr[0] + 1u;
-    if (lit4) {
-        word = src4(D.src, addr[0]);  // long literal run outside the staged window
-    } else {
-        const uint8_t *lds = (const uint8_t *)&L;
+    // fetch: LDS for every byte (invalid addresses read 0), HBM only if a lane needs it
+    const uint8_t *lds = (const uint8_t *)&L;
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t lv = lds[lad[j] & 0xFFFFu];   // unconditional (out of range reads 0)
+        v[j] = lad[j] != 0xFFFFFFFFu ? lv : 0u;
+    }
+    if (__any(anyg)) {
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            uint32_t v = 0;
-            if (kind[j] == 1) v = lds[addr[j]];
-            else if (kind[j] == 2) {
-                if (isdst[j]) {
-                    gcu8 *pp = D.dst + addr[j];
-                    const uint32_t sh = (uint32_t)((uintptr_t)pp & 3u);
-                    v = (__builtin_nontemporal_load(
-                             (__attribute__((address_space(1))) const uint32_t *)(pp - sh)) >>
-                         (8 * sh)) & 0xFFu;
-                } else {
-                    v = D.src[addr[j]];
-                }
-            }
-            word |= v << (8 * j);
+            // one nontemporal byte load for both sources (history in dst must bypass
+            // this CU's L1; the literal in src does not care); idle lanes read src[0]
+            gcu8 *bp = gk[j] == 2u ? (gcu8 *)D.dst : D.src;
+            const uint32_t o = gk[j] != 0u ? pos[j] : 0u;
+            const uint32_t g = __builtin_nontemporal_load(bp + o);
+            v[j] = gk[j] != 0u ? g : v[j];
         }
     }
+    const uint32_t word = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
     wave_sync();
-    // store: ring and dst
+    // store: ring and dst (the whole-step case is uniform)
     gu8 *o8 = D.dst + q0;
-    if (q0 >= lo && q0 + 4u <= hi) {
+    if (lo == base && hi == base + kStep) {
         *(uint32_t *)&L.ring[q0 & (kRing - 1)] = word;
-        if ((((uintptr_t)o8) & 3u) == 0) {
+        if ((((uintptr_t)(D.dst + base)) & 3u) == 0) {
             *(__attribute__((address_space(1))) uint32_t *)o8 = word;
         } else {
 #pragma unroll

@@ -116,8 +116,16 @@ __device__ __forceinline__ void shift_bytes(const uint32_t (&L)[8], int d, uint3
 // SMALL: byte loads.  Otherwise (n >= 32): two unaligned 16-byte loads from the
 // clamped window, fixed up with ALU only (so the wave's vmcnt accounting stays
 // static in the pipelined loop).
+// fast (wave-uniform): every lane's window is known to lie inside [0, n).
 template <bool SMALL>
-__device__ __forceinline__ void load32(gcu8 *in, int n, int pos, uint32_t (&X)[8]) {
+__device__ __forceinline__ void load32(gcu8 *in, int n, int pos, uint32_t (&X)[8],
+                                       bool fast = false) {
+    if (!SMALL && fast) {
+        const uint4 a = gload16(in + (uint32_t)pos), b = gload16(in + ((uint32_t)pos + 16u));
+        X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w;
+        X[4] = b.x; X[5] = b.y; X[6] = b.z; X[7] = b.w;
+        return;
+    }
     if (SMALL) {
 #pragma unroll
         for (int k = 0; k < 8; k++) X[k] = 0;
@@ -225,18 +233,21 @@ struct Part {                        // C1 result of one chunk, finished by C2
     bool has, hashable, trunc1;
 };
 
-struct Prod {
-    uint32_t X1[8], X2[8], X3[8];    // own bytes of chunks s+1, s+2, s+3
-    uint32_t Y1[8], Y2[8];           // T-candidate bytes of chunks s+1, s+2
-    uint32_t E0[8], E1[8];           // second-stage candidate bytes of chunks s, s+1
-    uint32_t cT1, jL1, h1, cT2, jL2, h2;
-    Part q0, q1;
+// One parity of the producer pipeline (the step loop is unrolled by two, so no
+// register set is ever copied): X from A for B, Y/cT/jL/h from B for C1, q/E from
+// C1 for C2.
+struct PSet {
+    uint32_t X[8];                   // own bytes of the chunk B works on next
+    uint32_t Y[8];                   // T-candidate bytes
+    uint32_t E[8];                   // second-stage candidate bytes
+    uint32_t cT, jL, h;
+    Part q;
 };
 
 template <bool SMALL>
 __device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_t (&X)[8]) {
     const int pos = (k < B.nch ? 64 * k : 0) + lane - 4;
-    load32<SMALL>(B.in, B.n, pos, X);
+    load32<SMALL>(B.in, B.n, pos, X, k >= 1 && k < B.nch && 64 * k + 91 <= B.n);
 }
 
 // B(k): hash, table + in-chunk candidates, T fetch issue, ring copy
@@ -255,19 +266,24 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
     jL = hashable ? S.scr[hs] : 0xFFFFFFFFu;
     wave_sync();
     if (hashable) S.scr[hs] = 0xFFFFFFFFu;
-    // ring copy of this chunk (second-stage, match_end - 2 and literal source)
-    if (live && p < B.un) ((uint8_t *)S.ring)[p & (kRingE - 1)] = (uint8_t)X[1];
-    // T candidate bytes (issued now, consumed one step later)
-    const bool tryT = live && cT < p;
-    load32<SMALL>(B.in, B.n, tryT ? (int)cT - 4 : 0, Y);
+    // ring copy of this chunk (own bytes for C1, second stage, match_end - 2,
+    // literals); zero past the block end
+    if (live) ((uint8_t *)S.ring)[p & (kRingE - 1)] = p < B.un ? (uint8_t)X[1] : (uint8_t)0;
+    // T candidate bytes (issued now, consumed one step later).  Candidates below
+    // position 4 are skipped: their 4 bytes of backward context would start before
+    // the block and need the slow edge path (never-written slots read as 0).
+    const bool tryT = live && cT < p && cT >= 4u;
+    load32<SMALL>(B.in, B.n, tryT ? (int)cT - 4 : 0, Y, 64 * k + 91 <= B.n);
 }
 
 // C1(k): verify / measure 28 bytes / pick; issue the second-stage load
 template <bool SMALL>
-__device__ __forceinline__ void prod_measure(const Blk &B, int k, int lane, const uint32_t (&X)[8],
+__device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int k, int lane,
                                              const uint32_t (&Y)[8], uint32_t cT, uint32_t jL,
                                              uint32_t h, Part &R, uint32_t (&E)[8]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    uint32_t X[8];
+    ring32(S, p - 4u, X);            // own bytes in[p-4, p+28) (ring tail = 0 before 0)
     const bool live = k < B.nch;
     R.hashable = live && p + 5u <= B.un;
     const bool can = live && p >= 1u && p <= B.mstart && B.n >= kMinLength;
@@ -275,11 +291,17 @@ __device__ __forceinline__ void prod_measure(const Blk &B, int k, int lane, cons
     uint32_t Z[8];
 #pragma unroll
     for (int t = 0; t < 8; t++) Z[t] = (uint32_t)__shfl((int)X[t], (int)(jL & 63u), 64);
-    const bool okT = can && cT < p && Y[1] == X[1];
+    const bool okT = can && cT < p && cT >= 4u && Y[1] == X[1];
     const bool okL = can && jL < (uint32_t)lane && cL != cT && Z[1] == X[1];
     R.lim = can ? B.mlimit - p : 0u;
+#ifdef APE_EXP_ONE_EAGER
+    const bool pickL = okL && !okT;
+    const uint32_t lT = pickL ? 0u : (okT ? eager(X, Y) : 0u);
+    const uint32_t lL = pickL ? eager(X, Z) : 0u;
+#else
     const uint32_t lT = okT ? eager(X, Y) : 0u, lL = okL ? eager(X, Z) : 0u;
     const bool pickL = okL && (!okT || lL > lT || (lL == lT && cL > cT));
+#endif
     R.c = pickL ? cL : cT;
     R.len = pickL ? lL : lT;
     R.trunc1 = R.len >= kEagerLen && R.lim > kEagerLen;
@@ -287,7 +309,7 @@ __device__ __forceinline__ void prod_measure(const Blk &B, int k, int lane, cons
     R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
     R.has = okT || okL;
     R.h = h;
-    load32<SMALL>(B.in, B.n, R.trunc1 ? (int)(R.c + kEagerLen) : 0, E);
+    load32<SMALL>(B.in, B.n, R.trunc1 ? (int)(R.c + kEagerLen) : 0, E, 64 * k + 123 <= B.n);
 }
 
 // C2(k): finish the truncated lengths against the ring, hash match_end - 2 -> info
@@ -502,7 +524,7 @@ template <bool SMALL>
 __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, int lane,
                                              int *result) {
     STATS_DECL
-    Prod Pr;
+    PSet P0, P1;
     Cons C;
     C.q = 0;
     C.anchor = 0;
@@ -512,23 +534,13 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
     C.m_back = C.m_len = C.anchor0 = 0;
     const int nch = B.n >= kMinLength ? B.nch : 0;   // :584, shorter -> last literals only
 
-    if (wave == 1 && nch > 0) {  // prologue: A(0..2), B(0), B(1), C1(0)
-        uint32_t X0[8], Y0[8];
-        uint32_t cT0, jL0, h0;
-        prod_load<SMALL>(B, 0, lane, X0);
-        prod_load<SMALL>(B, 1, lane, Pr.X1);
-        prod_load<SMALL>(B, 2, lane, Pr.X2);
-        prod_lookup<SMALL>(S, B, 0, lane, X0, cT0, jL0, h0, Y0);
-        prod_lookup<SMALL>(S, B, 1, lane, Pr.X1, Pr.cT1, Pr.jL1, Pr.h1, Pr.Y1);
-        prod_measure<SMALL>(B, 0, lane, X0, Y0, cT0, jL0, h0, Pr.q0, Pr.E0);
-    }
-    __syncthreads();
-    for (int s = 0; s <= nch; s++) {
+    // one producer/consumer step; `cur` = set of parity s, `nxt` = parity s + 1
+    auto step = [&](int s, PSet &cur, PSet &nxt) {
         // ---- first half: producer A(s+3), B(s+2) | consumer walks chunk s-1 ----
         if (wave == 1) {
             if (s + 2 < nch) {
-                prod_load<SMALL>(B, s + 3, lane, Pr.X3);
-                prod_lookup<SMALL>(S, B, s + 2, lane, Pr.X2, Pr.cT2, Pr.jL2, Pr.h2, Pr.Y2);
+                prod_load<SMALL>(B, s + 3, lane, nxt.X);
+                prod_lookup<SMALL>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
             }
             STAT(5);
         } else if (s >= 1) {
@@ -541,20 +553,9 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         if (wave == 1) {
             if (s < nch) {
                 if (s + 1 < nch)
-                    prod_measure<SMALL>(B, s + 1, lane, Pr.X1, Pr.Y1, Pr.cT1, Pr.jL1, Pr.h1, Pr.q1,
-                                        Pr.E1);
-                prod_finish(S, B, s, lane, Pr.q0, Pr.E0);
-#pragma unroll
-                for (int t = 0; t < 8; t++) {
-                    Pr.X1[t] = Pr.X2[t];
-                    Pr.X2[t] = Pr.X3[t];
-                    Pr.Y1[t] = Pr.Y2[t];
-                    Pr.E0[t] = Pr.E1[t];
-                }
-                Pr.cT1 = Pr.cT2;
-                Pr.jL1 = Pr.jL2;
-                Pr.h1 = Pr.h2;
-                Pr.q0 = Pr.q1;
+                    prod_measure<SMALL>(S, B, s + 1, lane, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q,
+                                        nxt.E);
+                prod_finish(S, B, s, lane, cur.q, cur.E);
             }
             STAT(7);
         } else if (s >= 1) {
@@ -565,6 +566,20 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         STAT_ADD(10, 1);
         __syncthreads();
         if (wave == 1) STAT(8); else STAT(3);
+    };
+
+    if (wave == 1 && nch > 0) {  // prologue: A(0), A(1), B(0), A(2), B(1), C1(0)
+        prod_load<SMALL>(B, 0, lane, P0.X);
+        prod_load<SMALL>(B, 1, lane, P1.X);
+        prod_lookup<SMALL>(S, B, 0, lane, P0.X, P0.cT, P0.jL, P0.h, P0.Y);
+        prod_load<SMALL>(B, 2, lane, P0.X);
+        prod_lookup<SMALL>(S, B, 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
+        prod_measure<SMALL>(S, B, 0, lane, P0.Y, P0.cT, P0.jL, P0.h, P0.q, P0.E);
+    }
+    __syncthreads();
+    for (int s = 0; s <= nch; s += 2) {
+        step(s, P0, P1);
+        if (s + 1 <= nch) step(s + 1, P1, P0);
     }
     if (wave != 0) {
         STATS_FLUSH_TID(g_enc_stats, 64);
@@ -621,6 +636,7 @@ lz4_encode_kernel(BlockArgs a) {
     // table = 0 (the reference's memset state: position 0 for every hash)
     for (int i = tid; i < kHSize / 8; i += 128) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
     for (int i = tid; i < 256; i += 128) S.scr[i] = 0xFFFFFFFFu;
+    for (int i = tid; i < (int)(kRingE / 16); i += 128) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     if (B.n < kSmall) encode_block<true>(S, B, wave, lane, &a.result[b]);
     else encode_block<false>(S, B, wave, lane, &a.result[b]);
