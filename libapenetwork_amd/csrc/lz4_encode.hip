@@ -59,7 +59,14 @@ namespace {
 constexpr int kHLog = APE_LZ4_HLOG;
 constexpr int kHSize = 1 << kHLog;
 constexpr uint32_t kEagerLen = 28;   // match bytes measured by the producer
-constexpr uint32_t kRingE = 2048;    // recent input bytes (literals, stage 2, end-2)
+#ifndef APE_LZ4_ERING
+#define APE_LZ4_ERING 1024
+#endif
+constexpr uint32_t kRingE = APE_LZ4_ERING;  // recent input bytes (own, stage 2, end-2, literals)
+#ifndef APE_LZ4_SCRBITS
+#define APE_LZ4_SCRBITS 7
+#endif
+constexpr uint32_t kScr = 1u << APE_LZ4_SCRBITS;  // in-chunk candidate scratch entries
 constexpr int kSmall = 128;          // smaller blocks take the byte-load path
 
 constexpr uint32_t kEager2 = kEagerLen + 32;  // after the producer's second stage
@@ -73,7 +80,7 @@ struct __attribute__((aligned(16))) EncLds {
     uint16_t tab[kHSize];
     uint32_t ring[kRingE / 4];       // input byte x at ring byte (x mod kRingE)
     uint2 info[2][64];
-    uint32_t scr[256];               // producer scratch: earliest lane per low hash bits
+    uint32_t scr[kScr];              // producer scratch: earliest lane per low hash bits
     uint4 rec[64];                   // consumer: sequence records of the chunk being emitted
     uint32_t omap[16];               // consumer: owner map of a 64-byte output window
 };
@@ -260,7 +267,7 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
     const bool hashable = live && p + 5u <= B.un;
     h = hash5(X[1], X[2]);
     cT = S.tab[h];
-    const uint32_t hs = h & 255u;
+    const uint32_t hs = h & (kScr - 1u);
     if (hashable) atomicMin(&S.scr[hs], (uint32_t)lane);
     wave_sync();
     jL = hashable ? S.scr[hs] : 0xFFFFFFFFu;
@@ -635,7 +642,7 @@ lz4_encode_kernel(BlockArgs a) {
 
     // table = 0 (the reference's memset state: position 0 for every hash)
     for (int i = tid; i < kHSize / 8; i += 128) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
-    for (int i = tid; i < 256; i += 128) S.scr[i] = 0xFFFFFFFFu;
+    for (int i = tid; i < (int)kScr; i += 128) S.scr[i] = 0xFFFFFFFFu;
     for (int i = tid; i < (int)(kRingE / 16); i += 128) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     if (B.n < kSmall) encode_block<true>(S, B, wave, lane, &a.result[b]);
