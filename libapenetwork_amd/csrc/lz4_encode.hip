@@ -360,10 +360,54 @@ struct Cons {
     bool overflow;
     uint64_t walked, members;
     uint32_t m_back, m_len, anchor0;  // per member lane / at the step start
+    uint32_t an;         // per member lane: end of the previous member (or anchor0)
 };
 
-// first half: walk chunk k (no table writes)
-__device__ __forceinline__ void cons_walk(const EncLds &S, const Blk &B, int k, int lane, Cons &C) {
+// forward extension of the match at m (candidate cm) from L bytes on, with the
+// whole wave, 1 KiB per step; returns the full length (<= mlimit - m)
+__device__ __forceinline__ uint32_t extend_match(const Blk &B, uint32_t m, uint32_t cm, uint32_t L,
+                                                 int lane) {
+    const uint32_t lm = B.mlimit - m;
+    for (;;) {
+        const uint32_t kk = L + 16u * (uint32_t)lane;
+        uint32_t d = 0, at = 0;
+        if (kk < lm) {
+            uint32_t xb[4] = {0, 0, 0, 0}, yb[4] = {0, 0, 0, 0};
+            if (m + kk + 16u <= B.un) {
+                const uint4 x = gload16(B.in + (m + kk)), y = gload16(B.in + (cm + kk));
+                xb[0] = x.x; xb[1] = x.y; xb[2] = x.z; xb[3] = x.w;
+                yb[0] = y.x; yb[1] = y.y; yb[2] = y.z; yb[3] = y.w;
+            } else {
+#pragma unroll
+                for (uint32_t t = 0; t < 16u; t++) {
+                    if (m + kk + t < B.un) {
+                        xb[t >> 2] |= (uint32_t)B.in[m + kk + t] << (8 * (t & 3));
+                        yb[t >> 2] |= (uint32_t)B.in[cm + kk + t] << (8 * (t & 3));
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 3; t >= 0; t--) {
+                const uint32_t e = xb[t] ^ yb[t];
+                if (e) { d = 1; at = 4u * (uint32_t)t + (__builtin_ctz(e) >> 3); }
+            }
+        }
+        const uint64_t bad = __ballot(d != 0 || kk >= lm);
+        if (bad) {
+            const int fl = __builtin_ctzll(bad);
+            const uint32_t k2 = L + 16u * (uint32_t)fl;
+            L = k2 >= lm ? lm : k2 + lane_val(at, fl);
+            break;
+        }
+        L += 1024u;
+    }
+    return L > lm ? lm : L;
+}
+
+#ifdef APE_DBG_WALK
+__device__ int g_dbg_count;
+// the serial walk (debug reference for the parallel one)
+__device__ __forceinline__ void cons_walk_ref(const EncLds &S, const Blk &B, int k, int lane, Cons &C) {
     const uint32_t P = 64u * (uint32_t)k;
     C.walked = 0;
     C.members = 0;
@@ -437,6 +481,119 @@ __device__ __forceinline__ void cons_walk(const EncLds &S, const Blk &B, int k, 
     }
     C.q = q;
 }
+#endif
+
+// first half: walk chunk k (no table writes).
+// The greedy chain (:591-627: a position with a match jumps past it, any other
+// position is a literal).  The scalar unit hops over the match lanes only (ballot
+// mask, one v_readlane per member); everything else -- walked positions, catch-up
+// limits, the new anchor -- follows for all 64 lanes at once from the member set.
+// A match the producer could not finish (TRUNC) is extended with the whole wave.
+// APE_WALK_DOUBLING selects a variant that resolves the chain by pointer doubling
+// (ds_permute / ds_bpermute, six rounds): no scalar loop, but six LDS round trips.
+__device__ __forceinline__ void cons_walk(const EncLds &S, const Blk &B, int k, int lane, Cons &C) {
+    const uint32_t P = 64u * (uint32_t)k;
+    C.walked = 0;
+    C.members = 0;
+    C.anchor0 = C.anchor;
+#ifdef APE_EXP_NO_WALK
+    return;
+#endif
+    if (C.overflow || C.q >= P + 64u) return;
+#ifdef APE_DBG_WALK
+    Cons R = C;
+    cons_walk_ref(S, B, k, lane, R);
+    const uint32_t q0dbg = C.q;
+#endif
+    const uint2 iv = S.info[k & 1][lane];
+    const bool has = (iv.x & I_HAS) != 0u, trunc = (iv.x & I_TRUNC) != 0u;
+    uint32_t Lf = iv.x & 0xFFu;                          // forward match length
+    uint32_t q = C.q;
+#ifdef APE_WALK_DOUBLING
+    // one hop: a finished match jumps past its end, a literal to the next position,
+    // an unfinished match leaves the chunk (resolved below)
+    const uint32_t J0 = has ? (trunc ? 64u : umin((uint32_t)lane + Lf, 64u)) : (uint32_t)lane + 1u;
+    for (;;) {
+        const uint32_t rel = q - P;
+        uint32_t J = J0, m = (uint32_t)lane == rel ? 1u : 0u;
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            const bool in = J < 64u;
+            // marks that stay in the chunk go to lane J; all other lanes send 0 to lane 0
+            // (no hop lands on 0, and lane 0 keeps its own mark through the OR)
+            const bool go = m && in;
+            const uint32_t t = (uint32_t)__builtin_amdgcn_ds_permute((int)(go ? 4u * J : 0u), go ? 1 : 0);
+            const uint32_t Jn = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (in ? J : 0u)), (int)J);
+            m |= t;
+            J = in ? Jn : J;
+        }
+        C.members |= __ballot(m != 0u && has);
+        const uint64_t ex = __ballot(m != 0u && J0 >= 64u);   // the node that leaves
+        const int e = __builtin_ctzll(ex);
+        const uint32_t ve = lane_val(iv.x, e);
+        if (!(ve & I_TRUNC)) {            // a finished match, or the literal at 63
+            q = P + (uint32_t)e + ((ve & I_HAS) ? (ve & 0xFFu) : 1u);
+            break;
+        }
+        const uint32_t me = P + (uint32_t)e;
+        const uint32_t cm = me - (lane_val(iv.y, e) & 0xFFFFu);
+        const uint32_t Le = extend_match(B, me, cm, ve & 0xFFu, lane);
+        if (lane == e) Lf = Le;
+        q = me + Le;
+        if (q >= P + 64u) break;
+    }
+#else
+    const uint64_t Hm = __ballot(has);
+    const uint32_t Lh = has ? (trunc ? 0x80u : Lf) : 0u;   // hop; 0x80 = unfinished
+    uint32_t rel = q - P;
+    uint64_t M = 0;
+    for (;;) {
+        const uint64_t w = Hm >> rel;
+        if (w == 0) { rel = 64u; break; }
+        const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
+        const uint32_t h = lane_val(Lh, (int)j);
+        M |= 1ull << j;
+        if (h & 0x80u) {
+            const uint32_t me = P + j;
+            const uint32_t cm = me - (lane_val(iv.y, (int)j) & 0xFFFFu);
+            const uint32_t Le = extend_match(B, me, cm, lane_val(iv.x, (int)j) & 0xFFu, lane);
+            if ((uint32_t)lane == j) Lf = Le;
+            rel = j + Le;
+        } else {
+            rel = j + h;
+        }
+        if (rel >= 64u) break;
+    }
+    q = P + rel;
+    C.members = M;
+#endif
+    // catch-up limits: a member's backward extension stops at the previous end
+    const bool mem = (C.members >> lane) & 1ull;
+    const uint32_t p = P + (uint32_t)lane;
+    const uint32_t end = mem ? p + Lf : 0u;
+    const uint32_t imax = wave_incl_max(end);
+    const uint32_t pm = umax(wave_shr1(imax, 0u), C.anchor0);
+    const uint32_t bk = umin((iv.x >> 8) & 7u, p - pm);
+    C.m_back = bk;
+    C.m_len = Lf + bk;
+    C.an = pm;
+    C.anchor = umax(C.anchor0, lane_val(imax, 63));
+    // walked = every position from the walk start that no match of this chunk covers
+    C.walked = __ballot(p >= C.q && pm <= p);
+    C.q = q;
+#ifdef APE_DBG_WALK
+    {
+        const bool bad = R.walked != C.walked || R.members != C.members || R.q != C.q ||
+                         R.anchor != C.anchor ||
+                         __ballot(mem && (R.m_back != C.m_back || R.m_len != C.m_len)) != 0;
+        if (bad && lane == 0 && atomicAdd(&g_dbg_count, 1) < 8)
+            printf("walk k=%d q0=%u: W %llx/%llx M %llx/%llx q %u/%u anc %u/%u\n", k, q0dbg,
+                   (unsigned long long)R.walked, (unsigned long long)C.walked,
+                   (unsigned long long)R.members, (unsigned long long)C.members, R.q, C.q,
+                   R.anchor, C.anchor);
+    }
+#endif
+}
 
 // second half: table updates, then emission of chunk k's sequences
 __device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int lane, Cons &C) {
@@ -472,8 +629,7 @@ __device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int la
 #endif
     if (!C.members) return;
     const uint32_t ms = p - C.m_back;            // match start after catch-up
-    const uint32_t end = ms + C.m_len;
-    const uint32_t an = umax(wave_shr1(wave_incl_max(mem ? end : 0u), 0u), C.anchor0);
+    const uint32_t an = C.an;
     const uint32_t lit = mem ? ms - an : 0u;
     const uint32_t ml = C.m_len - kMinMatch;
     const uint32_t size = mem ? 1u + ext_bytes(lit) + lit + 2u + ext_bytes(ml) : 0u;
@@ -538,7 +694,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
     C.o = 0;
     C.overflow = false;
     C.walked = C.members = 0;
-    C.m_back = C.m_len = C.anchor0 = 0;
+    C.m_back = C.m_len = C.anchor0 = C.an = 0;
     const int nch = B.n >= kMinLength ? B.nch : 0;   // :584, shorter -> last literals only
 
     // one producer/consumer step; `cur` = set of parity s, `nxt` = parity s + 1
@@ -575,6 +731,12 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         if (wave == 1) STAT(8); else STAT(3);
     };
 
+#ifdef APE_EXP_PRIO_CONS
+    if (wave == 0) __builtin_amdgcn_s_setprio(APE_EXP_PRIO_CONS);
+#endif
+#ifdef APE_EXP_PRIO_PROD
+    if (wave == 1) __builtin_amdgcn_s_setprio(APE_EXP_PRIO_PROD);
+#endif
     if (wave == 1 && nch > 0) {  // prologue: A(0), A(1), B(0), A(2), B(1), C1(0)
         prod_load<SMALL>(B, 0, lane, P0.X);
         prod_load<SMALL>(B, 1, lane, P1.X);
