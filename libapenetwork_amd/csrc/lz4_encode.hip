@@ -78,7 +78,9 @@ constexpr uint32_t I_TRUNC = 1u << 11, I_HAS = 1u << 12, I_HASHABLE = 1u << 13,
 
 struct __attribute__((aligned(16))) EncLds {
     uint16_t tab[kHSize];
-    uint32_t ring[kRingE / 4];       // input byte x at ring byte (x mod kRingE)
+    // input byte x at ring byte (x mod kRingE); the first 64 bytes are mirrored
+    // after the end, so a 36-byte read never wraps (immediate LDS offsets)
+    uint32_t ring[kRingE / 4 + 16];
     uint2 info[2][64];
     uint32_t scr[kScr];              // producer scratch: earliest lane per low hash bits
     uint4 rec[64];                   // consumer: sequence records of the chunk being emitted
@@ -167,21 +169,38 @@ __device__ __forceinline__ uint32_t hash5(uint32_t x1, uint32_t b4) {
     return (uint32_t)((seq * 889523592379ULL) >> (40 - kHLog)) & (kHSize - 1);
 }
 
+// v_ffbl_b32 / v_ffbh_u32: lowest / highest set bit, 0xFFFFFFFF for 0 (inline asm
+// so that the compiler does not turn the zero case into compare + select)
+__device__ __forceinline__ uint32_t ffbl(uint32_t d) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(d));
+    return r;
+}
+__device__ __forceinline__ uint32_t ffbh(uint32_t d) {
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(d));
+    return r;
+}
+
+// first differing bit of dwords A[K0..K1) vs B (bit index from A[K0]'s bit 0), or
+// 0xFFFFFFFF: ffbl + saturating add + min3 per dword, no compares or selects
+template <int K0, int K1>
+__device__ __forceinline__ uint32_t first_diff_bit(const uint32_t (&A)[8], const uint32_t (&B)[8]) {
+    uint32_t m = ffbl(A[K0] ^ B[K0]);
+#pragma unroll
+    for (int k = K0 + 1; k < K1; k++)
+        m = umin(m, __builtin_elementwise_add_sat(ffbl(A[k] ^ B[k]), 32u * (uint32_t)(k - K0)));
+    return m;
+}
+
 // common length of X and Y from byte 4 (dword 1) on, up to kEagerLen
 __device__ __forceinline__ uint32_t eager(const uint32_t (&X)[8], const uint32_t (&Y)[8]) {
-    uint32_t len = kEagerLen;
-#pragma unroll
-    for (int k = 7; k >= 2; k--) {
-        const uint32_t d = X[k] ^ Y[k];
-        if (d) len = 4u * (uint32_t)(k - 1) + (__builtin_ctz(d) >> 3);
-    }
-    return len;
+    return umin((first_diff_bit<2, 8>(X, Y) >> 3) + 4u, kEagerLen);
 }
 
 // bytes equal just before the match (in[p-1] == in[c-1], ...), 0..4
 __device__ __forceinline__ uint32_t back4(uint32_t x0, uint32_t y0) {
-    const uint32_t d = x0 ^ y0;
-    return d ? (__builtin_clz(d) >> 3) : 4u;
+    return umin(ffbh(x0 ^ y0) >> 3, 4u);
 }
 
 __device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {  // bytes after a 15 nibble
@@ -199,17 +218,17 @@ __device__ __forceinline__ void put_len(gu8 *o, uint32_t v) {
 
 // 4 input bytes at x from the ring
 __device__ __forceinline__ uint32_t ring4(const EncLds &S, uint32_t x) {
-    const uint32_t w = x >> 2;
-    return __builtin_amdgcn_alignbyte(S.ring[(w + 1) & (kRingE / 4 - 1)],
-                                      S.ring[w & (kRingE / 4 - 1)], x & 3u);
+    const uint32_t *r = S.ring + ((x >> 2) & (kRingE / 4 - 1));
+    return __builtin_amdgcn_alignbyte(r[1], r[0], x & 3u);
 }
 
 // 32 input bytes at x from the ring
 __device__ __forceinline__ void ring32(const EncLds &S, uint32_t x, uint32_t (&O)[8]) {
-    const uint32_t w0 = x >> 2, sh = x & 3u;
+    const uint32_t *r = S.ring + ((x >> 2) & (kRingE / 4 - 1));
+    const uint32_t sh = x & 3u;
     uint32_t W[9];
 #pragma unroll
-    for (int k = 0; k < 9; k++) W[k] = S.ring[(w0 + k) & (kRingE / 4 - 1)];
+    for (int k = 0; k < 9; k++) W[k] = r[k];
 #pragma unroll
     for (int k = 0; k < 8; k++) O[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
 }
@@ -275,7 +294,11 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
     if (hashable) S.scr[hs] = 0xFFFFFFFFu;
     // ring copy of this chunk (own bytes for C1, second stage, match_end - 2,
     // literals); zero past the block end
-    if (live) ((uint8_t *)S.ring)[p & (kRingE - 1)] = p < B.un ? (uint8_t)X[1] : (uint8_t)0;
+    if (live) {
+        const uint8_t by = p < B.un ? (uint8_t)X[1] : (uint8_t)0;
+        ((uint8_t *)S.ring)[p & (kRingE - 1)] = by;
+        if (((64u * (uint32_t)k) & (kRingE - 1)) == 0u) ((uint8_t *)S.ring)[kRingE + lane] = by;
+    }
     // T candidate bytes (issued now, consumed one step later).  Candidates below
     // position 4 are skipped: their 4 bytes of backward context would start before
     // the block and need the slow edge path (never-written slots read as 0).
@@ -332,12 +355,7 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
 #endif
         uint32_t O[8];
         ring32(S, p + kEagerLen, O);             // own bytes p+28 .. p+60
-        uint32_t ext = 32;
-#pragma unroll
-        for (int t = 7; t >= 0; t--) {
-            const uint32_t d = O[t] ^ E[t];
-            if (d) ext = 4u * (uint32_t)t + (__builtin_ctz(d) >> 3);
-        }
+        const uint32_t ext = umin(first_diff_bit<0, 8>(O, E) >> 3, 32u);
         len = kEagerLen + ext;
         trunc = ext == 32u && R.lim > kEager2;
         if (len > R.lim) len = R.lim;
@@ -805,7 +823,7 @@ lz4_encode_kernel(BlockArgs a) {
     // table = 0 (the reference's memset state: position 0 for every hash)
     for (int i = tid; i < kHSize / 8; i += 128) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
     for (int i = tid; i < (int)kScr; i += 128) S.scr[i] = 0xFFFFFFFFu;
-    for (int i = tid; i < (int)(kRingE / 16); i += 128) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < (int)(kRingE / 16 + 4); i += 128) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     if (B.n < kSmall) encode_block<true>(S, B, wave, lane, &a.result[b]);
     else encode_block<false>(S, B, wave, lane, &a.result[b]);
