@@ -263,28 +263,38 @@ struct Part {                        // C1 result of one chunk, finished by C2
 // register set is ever copied): X from A for B, Y/cT/jL/h from B for C1, q/E from
 // C1 for C2.
 struct PSet {
-    uint32_t X[8];                   // own bytes of the chunk B works on next
+    uint32_t X[2];                   // own bytes in[p, p+8) of the chunk B works on next
     uint32_t Y[8];                   // T-candidate bytes
     uint32_t E[8];                   // second-stage candidate bytes
     uint32_t cT, jL, h;
     Part q;
 };
 
+// A(k): own bytes in[p, p+8) for the hash (0 past the block end)
 template <bool SMALL>
-__device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_t (&X)[8]) {
-    const int pos = (k < B.nch ? 64 * k : 0) + lane - 4;
-    load32<SMALL>(B.in, B.n, pos, X, k >= 1 && k < B.nch && 64 * k + 91 <= B.n);
+__device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_t (&X)[2]) {
+    const uint32_t pos = (k < B.nch ? 64u * (uint32_t)k : 0u) + (uint32_t)lane;
+    if (!SMALL && 64 * k + 72 <= B.n) {          // wave-uniform: the whole window is inside
+        const uint2 v = gload8(B.in + pos);
+        X[0] = v.x;
+        X[1] = v.y;
+        return;
+    }
+    X[0] = X[1] = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < 8u; t++)
+        if (pos + t < B.un) X[t >> 2] |= (uint32_t)B.in[pos + t] << (8 * (t & 3));
 }
 
 // B(k): hash, table + in-chunk candidates, T fetch issue, ring copy
 template <bool SMALL>
 __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int lane,
-                                            const uint32_t (&X)[8], uint32_t &cT, uint32_t &jL,
+                                            const uint32_t (&X)[2], uint32_t &cT, uint32_t &jL,
                                             uint32_t &h, uint32_t (&Y)[8]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const bool live = k < B.nch;
     const bool hashable = live && p + 5u <= B.un;
-    h = hash5(X[1], X[2]);
+    h = hash5(X[0], X[1]);
     cT = S.tab[h];
     const uint32_t hs = h & (kScr - 1u);
     if (hashable) atomicMin(&S.scr[hs], (uint32_t)lane);
@@ -295,7 +305,7 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
     // ring copy of this chunk (own bytes for C1, second stage, match_end - 2,
     // literals); zero past the block end
     if (live) {
-        const uint8_t by = p < B.un ? (uint8_t)X[1] : (uint8_t)0;
+        const uint8_t by = (uint8_t)X[0];
         ((uint8_t *)S.ring)[p & (kRingE - 1)] = by;
         if (((64u * (uint32_t)k) & (kRingE - 1)) == 0u) ((uint8_t *)S.ring)[kRingE + lane] = by;
     }
