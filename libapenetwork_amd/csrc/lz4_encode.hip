@@ -130,7 +130,8 @@ template <bool SMALL>
 __device__ __forceinline__ void load32(gcu8 *in, int n, int pos, uint32_t (&X)[8],
                                        bool fast = false) {
     if (!SMALL && fast) {
-        const uint4 a = gload16(in + (uint32_t)pos), b = gload16(in + ((uint32_t)pos + 16u));
+        gcu8 *q = in + (uint32_t)pos;   // saddr + voffset, +16 as the immediate offset
+        const uint4 a = gload16(q), b = gload16(q + 16);
         X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w;
         X[4] = b.x; X[5] = b.y; X[6] = b.z; X[7] = b.w;
         return;
@@ -146,7 +147,8 @@ __device__ __forceinline__ void load32(gcu8 *in, int n, int pos, uint32_t (&X)[8
         return;
     }
     const int ca = pos < 0 ? 0 : (pos > n - 32 ? n - 32 : pos);
-    const uint4 a = gload16(in + (uint32_t)ca), b = gload16(in + ((uint32_t)ca + 16u));
+    gcu8 *q = in + (uint32_t)ca;
+    const uint4 a = gload16(q), b = gload16(q + 16);
     const uint32_t L[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     if (ca == pos) {
 #pragma unroll
