@@ -36,6 +36,7 @@
 //   Two workgroup barriers per step keep the table reads of B (before the first)
 //   apart from the consumer's inserts (after it), so the output is deterministic.
 #include "lz4_gpu_internal.h"
+#include <type_traits>
 
 namespace apelz4 {
 
@@ -86,6 +87,16 @@ struct __attribute__((aligned(16))) EncLds {
     uint4 rec[64];                   // consumer: sequence records of the chunk being emitted
     uint32_t omap[16];               // consumer: owner map of a 64-byte output window
 };
+
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt at their maxima = no wait).  The
+// producer states its pipeline's waits explicitly: the compiler's own counter
+// analysis treats a load whose consumer sits in a skipped branch as still in flight
+// and then waits for every load before the register is reused.
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    static_assert(N >= 0 && N < 16, "vmcnt");
+    __builtin_amdgcn_s_waitcnt(N | (7 << 4) | (15 << 8));
+}
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -273,10 +284,10 @@ struct PSet {
 };
 
 // A(k): own bytes in[p, p+8) for the hash (0 past the block end)
-template <bool SMALL>
+template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_t (&X)[2]) {
     const uint32_t pos = (k < B.nch ? 64u * (uint32_t)k : 0u) + (uint32_t)lane;
-    if (!SMALL && 64 * k + 72 <= B.n) {          // wave-uniform: the whole window is inside
+    if (FAST || (!SMALL && 64 * k + 72 <= B.n)) {   // wave-uniform: the whole window is inside
         const uint2 v = gload8(B.in + pos);
         X[0] = v.x;
         X[1] = v.y;
@@ -288,8 +299,19 @@ __device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_
         if (pos + t < B.un) X[t >> 2] |= (uint32_t)B.in[pos + t] << (8 * (t & 3));
 }
 
+// T candidate bytes of chunk k (issued one step before C1 consumes them).  Candidates
+// below position 4 are skipped: their 4 bytes of backward context would start before
+// the block and need the slow edge path (never-written slots read as 0).
+template <bool SMALL, bool FAST = false>
+__device__ __forceinline__ void prod_fetch_t(const Blk &B, int k, int lane, uint32_t cT,
+                                             uint32_t (&Y)[8]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const bool tryT = k < B.nch && cT < p && cT >= 4u;
+    load32<SMALL>(B.in, B.n, tryT ? (int)cT - 4 : 0, Y, FAST || 64 * k + 91 <= B.n);
+}
+
 // B(k): hash, table + in-chunk candidates, T fetch issue, ring copy
-template <bool SMALL>
+template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int lane,
                                             const uint32_t (&X)[2], uint32_t &cT, uint32_t &jL,
                                             uint32_t &h, uint32_t (&Y)[8]) {
@@ -314,12 +336,11 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
     // T candidate bytes (issued now, consumed one step later).  Candidates below
     // position 4 are skipped: their 4 bytes of backward context would start before
     // the block and need the slow edge path (never-written slots read as 0).
-    const bool tryT = live && cT < p && cT >= 4u;
-    load32<SMALL>(B.in, B.n, tryT ? (int)cT - 4 : 0, Y, 64 * k + 91 <= B.n);
+    prod_fetch_t<SMALL, FAST>(B, k, lane, cT, Y);
 }
 
 // C1(k): verify / measure 28 bytes / pick; issue the second-stage load
-template <bool SMALL>
+template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int k, int lane,
                                              const uint32_t (&Y)[8], uint32_t cT, uint32_t jL,
                                              uint32_t h, Part &R, uint32_t (&E)[8]) {
@@ -341,7 +362,10 @@ __device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int 
     const uint32_t lT = pickL ? 0u : (okT ? eager(X, Y) : 0u);
     const uint32_t lL = pickL ? eager(X, Z) : 0u;
 #else
-    const uint32_t lT = okT ? eager(X, Y) : 0u, lL = okL ? eager(X, Z) : 0u;
+    // measured unconditionally (selects, no branches): every lane reads Y, so the
+    // compiler sees the candidate load consumed on every path
+    const uint32_t eT = eager(X, Y), eL = eager(X, Z);
+    const uint32_t lT = okT ? eT : 0u, lL = okL ? eL : 0u;
     const bool pickL = okL && (!okT || lL > lT || (lL == lT && cL > cT));
 #endif
     R.c = pickL ? cL : cT;
@@ -351,7 +375,8 @@ __device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int 
     R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
     R.has = okT || okL;
     R.h = h;
-    load32<SMALL>(B.in, B.n, R.trunc1 ? (int)(R.c + kEagerLen) : 0, E, 64 * k + 123 <= B.n);
+    load32<SMALL>(B.in, B.n, R.trunc1 ? (int)(R.c + kEagerLen) : 0, E,
+                  FAST || 64 * k + 123 <= B.n);
 }
 
 // C2(k): finish the truncated lengths against the ring, hash match_end - 2 -> info
@@ -360,17 +385,14 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     uint32_t len = R.len;
     bool trunc = false;
-#ifdef APE_EXP_NO_STAGE2
-    if (false) {
-#else
-    if (R.trunc1) {
-#endif
+    {   // unconditional for the same reason as in C1
         uint32_t O[8];
         ring32(S, p + kEagerLen, O);             // own bytes p+28 .. p+60
         const uint32_t ext = umin(first_diff_bit<0, 8>(O, E) >> 3, 32u);
-        len = kEagerLen + ext;
-        trunc = ext == 32u && R.lim > kEager2;
-        if (len > R.lim) len = R.lim;
+        if (R.trunc1) {
+            len = umin(kEagerLen + ext, R.lim);
+            trunc = ext == 32u && R.lim > kEager2;
+        }
     }
     uint32_t e2 = 0;
     if (R.has && !trunc) {
@@ -726,40 +748,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
     C.walked = C.members = 0;
     C.m_back = C.m_len = C.anchor0 = C.an = 0;
     const int nch = B.n >= kMinLength ? B.nch : 0;   // :584, shorter -> last literals only
-
-    // one producer/consumer step; `cur` = set of parity s, `nxt` = parity s + 1
-    auto step = [&](int s, PSet &cur, PSet &nxt) {
-        // ---- first half: producer A(s+3), B(s+2) | consumer walks chunk s-1 ----
-        if (wave == 1) {
-            if (s + 2 < nch) {
-                prod_load<SMALL>(B, s + 3, lane, nxt.X);
-                prod_lookup<SMALL>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
-            }
-            STAT(5);
-        } else if (s >= 1) {
-            cons_walk(S, B, s - 1, lane, C);
-            STAT(0);
-        }
-        __syncthreads();
-        if (wave == 1) STAT(6); else STAT(4);
-        // ---- second half: producer C1(s+1), C2(s) | consumer table + emission of s-1 ----
-        if (wave == 1) {
-            if (s < nch) {
-                if (s + 1 < nch)
-                    prod_measure<SMALL>(S, B, s + 1, lane, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q,
-                                        nxt.E);
-                prod_finish(S, B, s, lane, cur.q, cur.E);
-            }
-            STAT(7);
-        } else if (s >= 1) {
-            cons_emit(S, B, s - 1, lane, C);
-            STAT(1);
-            STAT_ADD(11, __popcll(C.members));
-        }
-        STAT_ADD(10, 1);
-        __syncthreads();
-        if (wave == 1) STAT(8); else STAT(3);
-    };
+    const int nsteps = (nch + 2) & ~1;   // >= nch + 1 producer/consumer steps, even
 
 #ifdef APE_EXP_PRIO_CONS
     if (wave == 0) __builtin_amdgcn_s_setprio(APE_EXP_PRIO_CONS);
@@ -767,22 +756,82 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
 #ifdef APE_EXP_PRIO_PROD
     if (wave == 1) __builtin_amdgcn_s_setprio(APE_EXP_PRIO_PROD);
 #endif
-    if (wave == 1 && nch > 0) {  // prologue: A(0), A(1), B(0), A(2), B(1), C1(0)
-        prod_load<SMALL>(B, 0, lane, P0.X);
-        prod_load<SMALL>(B, 1, lane, P1.X);
-        prod_lookup<SMALL>(S, B, 0, lane, P0.X, P0.cT, P0.jL, P0.h, P0.Y);
-        prod_load<SMALL>(B, 2, lane, P0.X);
-        prod_lookup<SMALL>(S, B, 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
-        prod_measure<SMALL>(S, B, 0, lane, P0.Y, P0.cT, P0.jL, P0.h, P0.q, P0.E);
-    }
-    __syncthreads();
-    for (int s = 0; s <= nch; s += 2) {
-        step(s, P0, P1);
-        if (s + 1 <= nch) step(s + 1, P1, P0);
-    }
-    if (wave != 0) {
+    // The two roles run separate loops (same number of barriers: 1 + 2 per step), so
+    // the compiler's memory-counter waits in each loop see only that role's loads
+    // and stores -- a shared loop merges both roles' in-flight operations at every
+    // join and turns the producer's pipelined waits into full ones.
+    if (wave == 1) {
+        // one producer step; `cur` = set of parity s, `nxt` = parity s + 1
+        auto pstep = [&](auto fast, int s, PSet &cur, PSet &nxt) {
+            constexpr bool F = decltype(fast)::value;
+            // first half: A(s+3), B(s+2).  In flight, oldest first: A(s+2), Y(s+1) x2,
+            // E(s) x2 -> A(s+2) has landed once at most 4 remain.
+            // Every stage runs on every step, past the last chunk too (it then loads
+            // from the block start and records nothing), so the number of loads per
+            // step -- and with it the waits -- is the same on every path.
+            vm_wait<4>();
+            prod_load<SMALL, F>(B, s + 3, lane, nxt.X);
+            prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
+            STAT(5);
+            __syncthreads();
+            STAT(6);
+            // second half: C1(s+1), C2(s).  In flight: Y(s+1) x2, E(s) x2, A(s+3),
+            // Y(s+2) x2 -> Y(s+1) at 5; after C1 issues E(s+1) x2, E(s) at 5.
+            vm_wait<5>();
+            prod_measure<SMALL, F>(S, B, s + 1, lane, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q, nxt.E);
+            vm_wait<5>();
+            prod_finish(S, B, s, lane, cur.q, cur.E);
+            STAT(7);
+            __syncthreads();
+            STAT(8);
+        };
+        if (nch > 0) {  // prologue: A(0), A(1), B(0), A(2), B(1), C1(0)
+            prod_load<SMALL>(B, 0, lane, P0.X);
+            prod_load<SMALL>(B, 1, lane, P1.X);
+            prod_lookup<SMALL>(S, B, 0, lane, P0.X, P0.cT, P0.jL, P0.h, P0.Y);
+            prod_load<SMALL>(B, 2, lane, P0.X);
+            prod_lookup<SMALL>(S, B, 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
+            prod_measure<SMALL>(S, B, 0, lane, P0.Y, P0.cT, P0.jL, P0.h, P0.q, P0.E);
+        }
+#ifndef APE_EXP_NO_PROLOGUE_WAIT
+        // nothing in flight at the loop entry, so the loop's counter waits depend only
+        // on its own issue order (once per block)
+        __builtin_amdgcn_s_waitcnt(0);
+#endif
+        __syncthreads();
+        // Steps whose three loads all lie inside the block (A(s+3): 64(s+3)+72 <= n,
+        // Y(s+2): 64(s+2)+91, E(s+1): 64(s+1)+123) run a loop without the edge paths;
+        // the last few steps run the general one.
+        const int nfast = SMALL ? 0 : umin((uint32_t)(B.n >= 264 ? ((B.n - 264) / 64 + 1) & ~1 : 0),
+                                           (uint32_t)nsteps);
+        int s = 0;
+        for (; s < nfast; s += 2) {   // no conditional step: see pstep
+            pstep(std::true_type{}, s, P0, P1);
+            pstep(std::true_type{}, s + 1, P1, P0);
+        }
+        for (; s < nsteps; s += 2) {
+            pstep(std::false_type{}, s, P0, P1);
+            pstep(std::false_type{}, s + 1, P1, P0);
+        }
         STATS_FLUSH_TID(g_enc_stats, 64);
         return;
+    }
+    // consumer: walk / table + emission of chunk s-1 during producer step s
+    __syncthreads();
+    for (int s = 0; s < nsteps; s++) {
+        const bool work = s >= 1 && s <= nch;
+        if (work) cons_walk(S, B, s - 1, lane, C);
+        STAT(0);
+        __syncthreads();
+        STAT(4);
+        if (work) {
+            cons_emit(S, B, s - 1, lane, C);
+            STAT_ADD(11, __popcll(C.members));
+        }
+        STAT(1);
+        STAT_ADD(10, 2);
+        __syncthreads();
+        STAT(3);
     }
     // ---- last literals (:732-751) ----
     if (!C.overflow) {
