@@ -674,7 +674,9 @@ __device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int la
             e2ok = true;
         }
     }
-    wave_sync();
+    // LDS operations of one wave complete in order: the walked-position inserts
+    // above land before these (compiler barrier only, no counter wait)
+    __builtin_amdgcn_sched_barrier(0);
     if (e2ok) S.tab[e2h] = (uint16_t)(p + fwd - 2u);
 #ifdef APE_EXP_NO_EMIT
     C.members = 0;
@@ -693,14 +695,18 @@ __device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int la
     }
     // Gather: lane L of window w produces output byte w + L.  Its sequence is the
     // last member starting at or before it (owner map + prefix max).
+    // (one wave's LDS operations complete in order, so the owner-map writes, the
+    // read-back and the clearing need no counter waits between them; omap is all
+    // zero between windows)
     if (mem) S.rec[lane] = make_uint4(ex, an, lit, ml | ((iv.y & 0xFFFFu) << 16));
     gu8 *out = B.dst + C.o;
     for (uint32_t w = 0; w < tot; w += 64u) {
-        if (lane < 16) S.omap[lane] = 0u;
-        wave_sync();
-        if (mem && ex > w && ex < w + 64u) ((uint8_t *)S.omap)[ex - w] = (uint8_t)(lane + 1);
-        wave_sync();
+        const bool mark = mem && ex > w && ex < w + 64u;
+        if (mark) ((uint8_t *)S.omap)[ex - w] = (uint8_t)(lane + 1);
+        __builtin_amdgcn_sched_barrier(0);
         const uint32_t mk = ((const uint8_t *)S.omap)[lane];
+        __builtin_amdgcn_sched_barrier(0);
+        if (mark) ((uint8_t *)S.omap)[ex - w] = 0;
         const uint64_t cov = __ballot(mem && ex <= w);   // member 0 starts at 0
         const uint32_t carry = 64u - (uint32_t)__clzll((long long)cov);
         const uint32_t own = umax(wave_incl_max(mk), carry) - 1u;
@@ -730,7 +736,6 @@ __device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int la
             }
             out[b] = (uint8_t)v;
         }
-        wave_sync();
     }
     C.o += tot;
 }
@@ -885,6 +890,7 @@ lz4_encode_kernel(BlockArgs a) {
     for (int i = tid; i < kHSize / 8; i += 128) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
     for (int i = tid; i < (int)kScr; i += 128) S.scr[i] = 0xFFFFFFFFu;
     for (int i = tid; i < (int)(kRingE / 16 + 4); i += 128) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
+    if (tid < 16) S.omap[tid] = 0u;
     __syncthreads();
     if (B.n < kSmall) encode_block<true>(S, B, wave, lane, &a.result[b]);
     else encode_block<false>(S, B, wave, lane, &a.result[b]);
