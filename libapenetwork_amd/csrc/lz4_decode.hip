@@ -51,9 +51,7 @@ struct __attribute__((aligned(16))) WaveLds {
     uint32_t own[kStep / 4];     // owner map of the current step (u8 per byte)
 };
 
-// per-lane speculative parse result (packed)
-constexpr uint32_t F_TERM = 1u << 8;   // final literals by input position, or ml error
-constexpr uint32_t F_CPLX = 1u << 9;   // needs the scalar path
+
 
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
@@ -206,20 +204,22 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const bool cx = lit == 15u || (mlx && e == 255u && !mlerr);
     const uint32_t ml = mlx ? 15u + e : mn;
     const int q = ipo + (mlx ? 1 : 0);           // next token
-    const uint32_t info = (uint32_t)(q - P) | ((fin_in || mlerr) ? F_TERM : 0u) | (cx ? F_CPLX : 0u);
+    // hop to the next token (relative to P); a final / failing sequence ends the
+    // chain (kHopTerm), a complex token ends it before itself (kHopCplx)
+    constexpr uint32_t kHopTerm = 0x80u, kHopCplx = 0xC0u;
+    const uint32_t hop = cx ? kHopCplx : ((fin_in || mlerr) ? kHopTerm : (uint32_t)(q - P));
 
-    // follow the chain from P (scalar)
-    uint32_t c = 0;
+    // follow the chain from P (scalar: one v_readlane per sequence, 4 instructions)
+    uint32_t c = 0, last = 0;
     uint64_t M = 0;
-    cplx = false;
-    for (;;) {
-        if (c >= 64u) break;
-        const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)c);
-        if (v & F_CPLX) { cplx = true; break; }
+    do {
+        last = c;
         M |= 1ull << c;
-        if (v & F_TERM) break;
-        c = v & 0xFFu;
-    }
+        c = (uint32_t)__builtin_amdgcn_readlane((int)hop, (int)c);
+    } while (c < 64u);
+    cplx = c == kHopCplx;
+    if (cplx) M &= ~(1ull << last);           // the complex token is not a member
+    if (c >= kHopTerm) c = last;              // (P is not advanced past a final token)
     // output positions, checks in the reference's order
     const bool mem = (M >> lane) & 1ull;
     const uint32_t ob = mem ? (fin_in ? lit : lit + ml + kMinMatch) : 0u;
@@ -487,7 +487,11 @@ lz4_decode_kernel(BlockArgs a) {
         wave_sync();
         const uint32_t bend = op;
         const uint32_t d_out = lane < nd ? L.desc[lane].y : 0u;
+#ifdef APE_DEXP_NOCOPY
+        for (uint32_t base = bend; base < bend; base += kStep) {
+#else
         for (uint32_t base = bstart & ~(uint32_t)(kStep - 1); base < bend; base += kStep) {
+#endif
             const uint32_t lo = base > bstart ? base : bstart;
             const uint32_t hi = base + kStep < bend ? base + kStep : bend;
             if (lo - gdone > (uint32_t)(kRing / 2)) {
