@@ -27,6 +27,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -89,6 +91,153 @@ def pmc_traffic(kernel, blocks):
         return None
 
 
+def e2e_bench(args):
+    """Host -> GPU -> host rate of the socket path (BASELINE config 5 / north_star e2e).
+
+    Compress (TX): pinned host blocks --H2D--> encode --> framed stream
+    [le32 c][block]... (frame_offsets + frame_pack) --D2H--> pinned host stream.
+    Decompress (RX): pinned framed stream --H2D--> decode straight out of the frames
+    --D2H--> pinned host blocks.  Chunks of `--e2e-chunk` blocks rotate over three
+    streams, each with its own device buffers (stream order protects their reuse), so
+    copies in both directions overlap the kernels.  Rates are
+    uncompressed bytes / wall time.  Never the headline `value`.
+    """
+    import torch
+
+    import libapenetwork_amd as amd
+
+    torch.cuda.set_device(0)
+    if amd.gpu_init() != 0:
+        raise SystemExit("GPU codec unavailable: %s" % amd.gpu_last_error())
+    n, nb, ch = args.block_size, args.e2e_blocks, args.e2e_chunk
+    nch = (nb + ch - 1) // ch
+    slot = (amd.compressBound(n) + 15) // 16 * 16
+    kind = 1 if args.kind == "comp" else 0
+    t0 = time.time()
+    h_src = torch.empty((nb, n), dtype=torch.uint8, pin_memory=True)
+    h_frames = torch.empty(nb * (slot + 4), dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty((nb, n), dtype=torch.uint8, pin_memory=True)
+    log("[e2e] pinned %.1f GiB host in %.1f s" % ((2 * nb * n + nb * (slot + 4)) / GIB,
+                                                  time.time() - t0))
+    NS = 3
+    streams = [torch.cuda.Stream() for _ in range(NS)]
+    bufs = []
+    for _ in range(NS):
+        bufs.append({
+            "src": torch.empty((ch, n), dtype=torch.uint8, device="cuda"),
+            "comp": torch.empty((ch, slot), dtype=torch.uint8, device="cuda"),
+            "csz": torch.zeros(ch, dtype=torch.int32, device="cuda"),
+            "off": torch.zeros(ch + 1, dtype=torch.int64, device="cuda"),
+            "frames": torch.empty(ch * (slot + 4), dtype=torch.uint8, device="cuda"),
+            "out": torch.empty((ch, n), dtype=torch.uint8, device="cuda"),
+            "res": torch.zeros(ch, dtype=torch.int32, device="cuda"),
+            "sizes": torch.full((ch,), n, dtype=torch.int32, device="cuda"),
+            "tot": torch.zeros(1, dtype=torch.int64, pin_memory=True),
+        })
+    for b in bufs:
+        b["scratch"] = amd.frame_offsets(b["csz"], b["off"])   # allocate scratch once
+    # input blocks: generated on the device, copied to pinned host memory (untimed)
+    for c in range(nch):
+        lo, hi = c * ch, min(nb, (c + 1) * ch)
+        amd.synth_blocks(bufs[0]["src"][:hi - lo], n, lo, kind)
+        h_src[lo:hi].copy_(bufs[0]["src"][:hi - lo])
+    torch.cuda.synchronize()
+
+    # plain pinned copy rates over one chunk (the PCIe ceiling of both directions)
+    probe = bufs[0]["src"]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record()
+    probe.copy_(h_src[:ch], non_blocking=True)
+    ev[1].record()
+    h_out[:ch].copy_(probe, non_blocking=True)
+    ev[2].record()
+    torch.cuda.synchronize()
+    h2d = ch * n / (ev[0].elapsed_time(ev[1]) * 1e-3) / 1e9
+    d2h = ch * n / (ev[1].elapsed_time(ev[2]) * 1e-3) / 1e9
+
+    def run_tx():
+        chunk_frames = []        # (host byte offset, bytes, host copy of offsets)
+        pos, pending = 0, None
+        for c in range(nch + 1):
+            if c < nch:
+                lo, hi = c * ch, min(nb, (c + 1) * ch)
+                b, s = bufs[c % NS], streams[c % NS]
+                with torch.cuda.stream(s):
+                    k = hi - lo
+                    b["src"][:k].copy_(h_src[lo:hi], non_blocking=True)
+                    amd.compress_batch(b["src"][:k], b["sizes"][:k], b["comp"][:k], b["csz"][:k],
+                                       stream=s)
+                    amd.frame_offsets(b["csz"][:k], b["off"][:k + 1], b["scratch"], stream=s)
+                    amd.frame_pack(b["comp"][:k], b["csz"][:k], b["off"][:k + 1], b["frames"],
+                                   stream=s)
+                    b["tot"].copy_(b["off"][k:k + 1], non_blocking=True)
+                    b["tev"] = torch.cuda.Event()
+                    b["tev"].record(s)
+            if pending is not None:      # issue the previous chunk's D2H once its size is known
+                pc, pb, ps = pending
+                pb["tev"].synchronize()
+                t = int(pb["tot"].item())
+                with torch.cuda.stream(ps):
+                    h_frames[pos:pos + t].copy_(pb["frames"][:t], non_blocking=True)
+                chunk_frames.append((pos, t))
+                pos += t
+            pending = (c, bufs[c % NS], streams[c % NS]) if c < nch else None
+        torch.cuda.synchronize()
+        return chunk_frames, pos
+
+    def run_rx(chunk_frames, offs):
+        for c in range(nch):
+            lo, hi = c * ch, min(nb, (c + 1) * ch)
+            k = hi - lo
+            b, s = bufs[c % NS], streams[c % NS]
+            fpos, t = chunk_frames[c]
+            with torch.cuda.stream(s):
+                b["frames"][:t].copy_(h_frames[fpos:fpos + t], non_blocking=True)
+                b["off"][:k + 1].copy_(offs[c], non_blocking=True)
+                amd.decompress_frames(b["frames"], b["off"], b["out"][:k], b["res"][:k],
+                                      dst_caps=b["sizes"][:k], nblocks=k, stream=s)
+                h_out[lo:hi].copy_(b["out"][:k], non_blocking=True)
+        torch.cuda.synchronize()
+
+    run_tx()                                   # warm-up
+    t0 = time.perf_counter()
+    chunk_frames, total = run_tx()
+    t_tx = time.perf_counter() - t0
+    # the receiver's frame offsets (from the headers; taken from the TX side, untimed)
+    offs = []
+    for c in range(nch):
+        k = min(nb, (c + 1) * ch) - c * ch
+        fpos, t = chunk_frames[c]
+        o = np.zeros(k + 1, dtype=np.int64)
+        fb = h_frames[fpos:fpos + t].numpy()
+        p = 0
+        for i in range(k):
+            o[i] = p
+            p += 4 + int(fb[p]) + (int(fb[p + 1]) << 8) + (int(fb[p + 2]) << 16) + (int(fb[p + 3]) << 24)
+        o[k] = p
+        offs.append(torch.from_numpy(o).pin_memory())
+    run_rx(chunk_frames, offs)                 # warm-up
+    t0 = time.perf_counter()
+    run_rx(chunk_frames, offs)
+    t_rx = time.perf_counter() - t0
+    ok = bool(torch.equal(h_out, h_src))
+    byt = nb * n
+    line = {
+        "metric": "LZ4 GiB/s end-to-end host->GPU->host (pinned H2D + kernels + D2H), socket path",
+        "value": round(byt / (t_tx + t_rx) / GIB, 2), "unit": "GiB/s", "n_gpus": 1,
+        "higher_is_better": True, "dtype": "u8",
+        "data": "synthetic (SURVEY App. C gen_%s)" % args.kind,
+        "config": {"workload": "%d x %d KiB blocks, chunks of %d over %d streams" % (
+            nb, n >> 10, ch, NS)},
+        "compress_e2e_GiBps": round(byt / t_tx / GIB, 2),
+        "decompress_e2e_GiBps": round(byt / t_rx / GIB, 2),
+        "framed_bytes": int(total), "ratio": round(byt / (total - 4 * nb), 4),
+        "pcie_h2d_GBps": round(h2d, 1), "pcie_d2h_GBps": round(d2h, 1),
+        "verified": ok,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,7 +249,13 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-sample", type=int, default=64)
+    ap.add_argument("--e2e", action="store_true",
+                    help="host->GPU->host socket-path rate instead of the device-resident line")
+    ap.add_argument("--e2e-blocks", type=int, default=1 << 17)
+    ap.add_argument("--e2e-chunk", type=int, default=1 << 14)
     args = ap.parse_args()
+    if args.e2e:
+        return e2e_bench(args)
 
     import torch
 

@@ -85,6 +85,28 @@ int APE_LZ4_decompress_safe_batch_strided_dev(const char *d_src, size_t src_stri
                                               const int *d_maxDecompressedSize,
                                               int *d_result, int nblocks, void *stream);
 
+/* ---- framed stream of independent blocks (socket path) ----
+ * The reference socket stream frames each LZ4 block as [int32 size][block]
+ * (ref src/ape_socket.c:813-850) with chained blocks; this batched form keeps
+ * the frame layout (little-endian size) with independent blocks, back to back.
+ *   frame_offsets : d_off[i] = sum_{j<i} (4 + d_compressedSize[j]) for i <= N
+ *                   (d_off has N + 1 entries, d_off[N] = stream length);
+ *                   d_scratch = APE_LZ4_frame_scratch_size(N) bytes of device memory
+ *   frame_pack    : compressed slots (block i at d_comp + i*comp_stride) -> frames
+ *   decompress_safe_frames : block i read from d_frames + d_off[i] (size from its
+ *                   header), decoded to d_dst + i*dst_stride; results as
+ *                   APE_LZ4_decompress_safe. */
+size_t APE_LZ4_frame_scratch_size(int nblocks);
+int APE_LZ4_frame_offsets_dev(const int *d_compressedSize, long long *d_off, void *d_scratch,
+                              int nblocks, void *stream);
+int APE_LZ4_frame_pack_strided_dev(const char *d_comp, size_t comp_stride,
+                                   const int *d_compressedSize, const long long *d_off,
+                                   char *d_frames, int nblocks, void *stream);
+int APE_LZ4_decompress_safe_frames_dev(const char *d_frames, const long long *d_off,
+                                       char *d_dst, size_t dst_stride,
+                                       const int *d_maxDecompressedSize, int *d_result,
+                                       int nblocks, void *stream);
+
 /* ---- host-buffer batch (socket / ape_buffer path): pinned staging, H2D,
  * kernel, D2H on an internal stream; synchronous.  h_result as above. */
 int APE_LZ4_compress_batch_host(const char *const *h_src, const int *h_srcSize,

@@ -16,7 +16,7 @@ __all__ = [
     "lib", "versionNumber", "compressBound", "compress_default", "compress_fast",
     "decompress_safe", "decompress_safe_partial", "compress_batch", "decompress_batch",
     "decompress_partial_batch", "synth_blocks", "gpu_init", "gpu_last_error", "GpuError",
-    "MAX_BLOCK", "ERANGE",
+    "MAX_BLOCK", "ERANGE", "frame_offsets", "frame_pack", "decompress_frames",
 ]
 
 _HERE = _os.path.dirname(_os.path.abspath(__file__))
@@ -58,6 +58,10 @@ def lib():
             "APE_LZ4_compress_batch_strided_dev": (i, [p, sz, p, p, sz, p, p, i, p]),
             "APE_LZ4_decompress_safe_batch_strided_dev": (i, [p, sz, p, p, sz, p, p, i, p]),
             "APE_LZ4_synth_blocks_dev": (i, [p, sz, i, ll, i, i, p]),
+            "APE_LZ4_frame_scratch_size": (sz, [i]),
+            "APE_LZ4_frame_offsets_dev": (i, [p, p, p, i, p]),
+            "APE_LZ4_frame_pack_strided_dev": (i, [p, sz, p, p, p, i, p]),
+            "APE_LZ4_decompress_safe_frames_dev": (i, [p, p, p, sz, p, p, i, p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -175,3 +179,33 @@ def synth_blocks(dst, block_size, first_block, kind, stream=None):
     _check(lib().APE_LZ4_synth_blocks_dev(_ptr(dst), dst.stride(0), block_size, first_block,
                                           dst.shape[0], kind, _stream(stream)),
            "APE_LZ4_synth_blocks_dev")
+
+
+# ---- framed stream of independent blocks (include/ape_lz4_gpu.h, socket path) ----
+def frame_offsets(comp_sizes, offsets, scratch=None, stream=None):
+    """offsets (int64 [N+1] CUDA) <- exclusive scan of 4 + comp_sizes[i]; returns scratch."""
+    import torch
+    n = comp_sizes.shape[0]
+    if scratch is None:
+        nbytes = lib().APE_LZ4_frame_scratch_size(n)
+        scratch = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=comp_sizes.device)
+    _check(lib().APE_LZ4_frame_offsets_dev(_ptr(comp_sizes), _ptr(offsets), _ptr(scratch), n,
+                                           _stream(stream)), "APE_LZ4_frame_offsets_dev")
+    return scratch
+
+
+def frame_pack(comp, comp_sizes, offsets, frames, stream=None):
+    """Framed stream [le32 c][c bytes]... of the compressed rows of comp (uint8 [N, D])."""
+    n = comp_sizes.shape[0]
+    _check(lib().APE_LZ4_frame_pack_strided_dev(_ptr(comp), comp.stride(0), _ptr(comp_sizes),
+                                                _ptr(offsets), _ptr(frames), n, _stream(stream)),
+           "APE_LZ4_frame_pack_strided_dev")
+
+
+def decompress_frames(frames, offsets, dst, results, dst_caps=None, nblocks=None, stream=None):
+    """N x APE_LZ4_decompress_safe of the blocks of a framed stream into rows of dst."""
+    n = dst.shape[0] if nblocks is None else nblocks
+    _check(lib().APE_LZ4_decompress_safe_frames_dev(_ptr(frames), _ptr(offsets), _ptr(dst),
+                                                    dst.stride(0), _ptr(dst_caps), _ptr(results),
+                                                    n, _stream(stream)),
+           "APE_LZ4_decompress_safe_frames_dev")

@@ -435,9 +435,16 @@ lz4_decode_kernel(BlockArgs a) {
     const int lane = threadIdx.x;
 
     Dec D;
-    D.src = (gcu8 *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
     D.dst = (gu8 *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
-    D.csize = a.src_size[b];
+    if (a.frame_off) {   // framed stream: [le32 size][block] (lz4_frame.hip)
+        gcu8 *f = (gcu8 *)(a.src_base + a.frame_off[b]);
+        D.csize = (int)((uint32_t)f[0] | ((uint32_t)f[1] << 8) | ((uint32_t)f[2] << 16) |
+                        ((uint32_t)f[3] << 24));
+        D.src = f + 4;
+    } else {
+        D.src = (gcu8 *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
+        D.csize = a.src_size[b];
+    }
     D.cap = a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride;
     D.oexit = PARTIAL ? a.target[b] : 0;
     if (PARTIAL && D.oexit > (int64_t)D.cap - kMFLimit) D.oexit = (int64_t)D.cap - kMFLimit;

@@ -122,12 +122,19 @@ struct BlockArgs {
     const int *src_size;      // per-block input size
     const int *dst_cap;       // per-block capacity (nullable -> default)
     const int *target;        // partial decode target (nullable)
+    const long long *frame_off;  // decoder: blocks read from a framed stream at src_base
+                                 // (frame i = [le32 size][block] at src_base + frame_off[i])
     int *result;
     int nblocks;
 };
 
 hipError_t launch_decode(const BlockArgs &a, bool partial, hipStream_t s);
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s);
+hipError_t launch_frame_offsets(const int *csize, long long *off, long long *scratch, int n,
+                                hipStream_t s);
+int frame_scratch_elems(int n);
+hipError_t launch_frame_pack(const char *comp, size_t stride, const int *csize,
+                             const long long *off, char *frames, int n, hipStream_t s);
 hipError_t launch_synth(char *out, size_t stride, int n, long long first, int nblocks,
                         int kind, hipStream_t s);
 

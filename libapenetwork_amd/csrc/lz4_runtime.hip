@@ -302,6 +302,53 @@ int APE_LZ4_decompress_safe_batch_strided_dev(const char *d_src, size_t src_stri
     return finish_launch(launch_decode(a, false, (hipStream_t)stream), "lz4_decode_kernel");
 }
 
+// ---- framed stream of independent blocks (lz4_frame.hip) ----
+size_t APE_LZ4_frame_scratch_size(int nblocks) {
+    return nblocks < 0 ? 0 : (size_t)frame_scratch_elems(nblocks) * sizeof(long long);
+}
+
+int APE_LZ4_frame_offsets_dev(const int *d_compressedSize, long long *d_off,
+                              void *d_scratch, int nblocks, void *stream) {
+    if (nblocks < 0 || !d_compressedSize || !d_off || !d_scratch) return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    return finish_launch(launch_frame_offsets(d_compressedSize, d_off, (long long *)d_scratch,
+                                              nblocks, (hipStream_t)stream),
+                         "frame offsets");
+}
+
+int APE_LZ4_frame_pack_strided_dev(const char *d_comp, size_t comp_stride,
+                                   const int *d_compressedSize, const long long *d_off,
+                                   char *d_frames, int nblocks, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_comp || !d_compressedSize || !d_off || !d_frames)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    return finish_launch(launch_frame_pack(d_comp, comp_stride, d_compressedSize, d_off,
+                                           d_frames, nblocks, (hipStream_t)stream),
+                         "frame pack");
+}
+
+int APE_LZ4_decompress_safe_frames_dev(const char *d_frames, const long long *d_off,
+                                       char *d_dst, size_t dst_stride,
+                                       const int *d_maxDecompressedSize, int *d_result,
+                                       int nblocks, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_frames || !d_off || !d_dst || !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    if (!d_maxDecompressedSize && dst_stride > 0x7FFFFFFF) return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    BlockArgs a{};
+    a.src_base = d_frames;
+    a.frame_off = d_off;
+    a.dst_base = d_dst;
+    a.dst_stride = dst_stride;
+    a.dst_cap = d_maxDecompressedSize;
+    a.result = d_result;
+    a.nblocks = nblocks;
+    return finish_launch(launch_decode(a, false, (hipStream_t)stream), "lz4_decode_kernel");
+}
+
 int APE_LZ4_compress_batch_host(const char *const *h_src, const int *h_srcSize,
                                 char *const *h_dst, const int *h_dstCap, int *h_result,
                                 int nblocks) {
