@@ -238,6 +238,64 @@ def e2e_bench(args):
     print(json.dumps(line), flush=True)
 
 
+def rand4k_bench(args):
+    """BASELINE config 2: 256K x 4 KiB random blocks, decompress only, 1 MI355X.
+
+    The blocks are generated (App. C gen_rand) and compressed once on the device
+    (untimed; the reference emits 4114 bytes for every such block -- our encoder's
+    sizes are reported beside it), then each step decodes all of them."""
+    import torch
+
+    import libapenetwork_amd as amd
+
+    torch.cuda.set_device(0)
+    if amd.gpu_init() != 0:
+        raise SystemExit("GPU codec unavailable: %s" % amd.gpu_last_error())
+    n, nb = 4096, args.rand4k_blocks
+    slot = (amd.compressBound(n) + 15) // 16 * 16
+    src = torch.empty((nb, n), dtype=torch.uint8, device="cuda")
+    amd.synth_blocks(src, n, 0, 0)
+    sizes = torch.full((nb,), n, dtype=torch.int32, device="cuda")
+    comp = torch.empty((nb, slot), dtype=torch.uint8, device="cuda")
+    csz = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    amd.compress_batch(src, sizes, comp, csz)
+    out = torch.empty((nb, n), dtype=torch.uint8, device="cuda")
+    res = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        amd.decompress_batch(comp, csz, out, res, dst_caps=sizes, stream=stream)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e in evs:
+        e[0].record(stream)
+        amd.decompress_batch(comp, csz, out, res, dst_caps=sizes, stream=stream)
+        e[1].record(stream)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / args.steps
+    ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    ok = bool((res == n).all().item()) and bool(torch.equal(out, src))
+    c = csz.to(torch.int64)
+    cbytes = int(c.sum().item())
+    alg = nb * n + cbytes
+    line = {
+        "metric": "LZ4 GiB/s decompress-only, 256K x 4 KiB random blocks (BASELINE config 2)",
+        "value": round(nb * n / (wall) / GIB, 2), "unit": "GiB/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall * 1e3, 3),
+        "higher_is_better": True, "dtype": "u8", "data": "synthetic (SURVEY App. C gen_rand)",
+        "config": {"workload": "%d x 4 KiB random blocks, decompress only" % nb},
+        "comp_bytes_min": int(c.min().item()), "comp_bytes_max": int(c.max().item()),
+        "reference_comp_bytes": 4114, "verified": ok,
+        "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "kernel": "lz4_decode_kernel", "bytes_per_launch": alg,
+                     "avg_launch_ms": round(ms, 3)},
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -253,9 +311,14 @@ def main():
                     help="host->GPU->host socket-path rate instead of the device-resident line")
     ap.add_argument("--e2e-blocks", type=int, default=1 << 17)
     ap.add_argument("--e2e-chunk", type=int, default=1 << 14)
+    ap.add_argument("--rand4k", action="store_true",
+                    help="BASELINE config 2: decompress-only over 4 KiB random blocks")
+    ap.add_argument("--rand4k-blocks", type=int, default=1 << 18)
     args = ap.parse_args()
     if args.e2e:
         return e2e_bench(args)
+    if args.rand4k:
+        return rand4k_bench(args)
 
     import torch
 
