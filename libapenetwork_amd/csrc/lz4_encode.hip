@@ -176,10 +176,15 @@ __device__ __forceinline__ void load32(gcu8 *in, int n, int pos, uint32_t (&X)[8
     }
 }
 
-// the reference's hash of the 5 bytes at p (x1 = in[p..p+3], b4 = in[p+4])
+// Hash of the 5 bytes at p (x1 = in[p..p+3], b4 = in[p+4]) into kHLog bits.  The
+// reference multiplies the 40-bit sequence by 889523592379 (:456-473), which needs
+// quarter-rate 32-bit multiplies here; any hash gives a valid stream, so this one
+// uses two full-rate 24 x 24-bit multiplies (v_mul_u32_u24) of bytes 0-2 and
+// bytes 3-4.  Same ratio on the App. C data (tools/enc_model.c: 3.1613 vs 3.1600).
 __device__ __forceinline__ uint32_t hash5(uint32_t x1, uint32_t b4) {
-    const uint64_t seq = (uint64_t)x1 | ((uint64_t)(b4 & 0xFFu) << 32);
-    return (uint32_t)((seq * 889523592379ULL) >> (40 - kHLog)) & (kHSize - 1);
+    const uint32_t lo = x1 & 0xFFFFFFu, hi = (x1 >> 24) | ((b4 & 0xFFu) << 8);
+    // (__umul24 returns int: do the sum and the shift unsigned)
+    return ((uint32_t)__umul24(lo, 0x9E3779u) + (uint32_t)__umul24(hi, 0xC2B2AEu)) >> (32 - kHLog);
 }
 
 // v_ffbl_b32 / v_ffbh_u32: lowest / highest set bit, 0xFFFFFFFF for 0 (inline asm

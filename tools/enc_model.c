@@ -24,6 +24,17 @@ static uint64_t rd64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v;
 
 static int ext(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
 
+/* hash variants for model2: 0 = reference 5-byte multiplicative, 1 = two 24-bit
+ * multiplies (full-rate on CDNA: v_mul_u32_u24) */
+static int g_hash = 0;
+static uint32_t hsh(const uint8_t *p, int hlog) {
+    if (g_hash == 0) return (uint32_t)((rd64(p) * 889523592379ULL) >> (40 - hlog)) & ((1u << hlog) - 1);
+    uint32_t x = rd32(p), b4 = p[4];
+    uint32_t lo = x & 0xFFFFFF, hi = (x >> 24) | (b4 << 8);
+    uint32_t v = lo * 0x9E3779u + hi * 0xC2B2AEu;   /* 24-bit x 24-bit, low 32 bits */
+    return v >> (32 - hlog);
+}
+
 static long model(const uint8_t *in, int n, int hlog, int insert, int R, int inround, int back)
 {
     const int H = 1 << hlog;
@@ -104,7 +115,7 @@ static long model2(const uint8_t *in, int n, int hlog, int R, int sb, int bcap, 
         const int P = p, r1 = P + R < n ? P + R : n;
         for (int i = 0; i < (1 << sb); i++) scr[i] = -1;
         for (int q = P; q < r1; q++) {
-            hh[q - P] = (q + 8 <= n) ? (uint32_t)((rd64(in + q) * 889523592379ULL) >> (40 - hlog)) & (H - 1) : 0;
+            hh[q - P] = (q + 8 <= n) ? hsh(in + q, hlog) : 0;
             cand[q - P] = tab[hh[q - P]];
             int k = hh[q - P] & ((1 << sb) - 1);
             cand2[q - P] = -1;
@@ -138,7 +149,7 @@ static long model2(const uint8_t *in, int n, int hlog, int R, int sb, int bcap, 
             }
         }
         for (int i = 0; i < nw; i++) if (walked[i] <= n - 5 && walked[i] < r1) tab[hh[walked[i] - P]] = walked[i];
-        if (end2) for (int i = 0; i < ne; i++) if (ends[i] + 8 <= n) tab[(uint32_t)((rd64(in + ends[i]) * 889523592379ULL) >> (40 - hlog)) & (H - 1)] = ends[i];
+        if (end2) for (int i = 0; i < ne; i++) if (ends[i] + 8 <= n) tab[hsh(in + ends[i], hlog)] = ends[i];
     }
     int lit = n - anchor;
     out += 1 + ext(lit) + lit;
@@ -232,12 +243,17 @@ int main(int argc, char **argv)
     struct { int hlog, R, sb, bcap, end2; } Q[] = {
         {13, 64, 8, 4, 1}, {13, 64, 8, 4, 0}, {13, 64, 8, 0, 1}, {13, 64, 8, 64, 1}, {13, 64, 0, 4, 1},
         {12, 64, 8, 4, 1}, {13, 128, 8, 4, 1}, {13, 64, 6, 4, 1}, {14, 64, 8, 4, 1}};
-    for (unsigned k = 0; k < sizeof(Q) / sizeof(Q[0]); k++) {
+    for (unsigned k = 0; k < 2 * sizeof(Q) / sizeof(Q[0]); k++) {
+        g_hash = k >= sizeof(Q) / sizeof(Q[0]);
+        if (g_hash && k % (sizeof(Q) / sizeof(Q[0])) != 0) continue;
         long tot = 0;
         for (int b = 0; b < nb; b++)
-            tot += model2(buf + (size_t)b * n, n, Q[k].hlog, Q[k].R, Q[k].sb, Q[k].bcap, Q[k].end2);
-        printf("wave: hlog %d R %d scratch-bits %d back-cap %d end-2 %d        ratio %.4f\n", Q[k].hlog,
-               Q[k].R, Q[k].sb, Q[k].bcap, Q[k].end2, (double)n * nb / tot);
+            tot += model2(buf + (size_t)b * n, n, Q[k % (sizeof(Q) / sizeof(Q[0]))].hlog,
+                          Q[k % (sizeof(Q) / sizeof(Q[0]))].R, Q[k % (sizeof(Q) / sizeof(Q[0]))].sb,
+                          Q[k % (sizeof(Q) / sizeof(Q[0]))].bcap, Q[k % (sizeof(Q) / sizeof(Q[0]))].end2);
+        const unsigned kq = k % (sizeof(Q) / sizeof(Q[0]));
+        printf("wave: hash %d hlog %d R %d scratch-bits %d back-cap %d end-2 %d  ratio %.4f\n", g_hash,
+               Q[kq].hlog, Q[kq].R, Q[kq].sb, Q[kq].bcap, Q[kq].end2, (double)n * nb / tot);
     }
     struct { int hlog, R, lag, sb, bcap; } T3[] = {
         {13, 64, 0, 8, 4}, {13, 64, 1, 8, 4}, {13, 64, 2, 8, 4}, {12, 64, 0, 8, 4}, {12, 64, 1, 8, 4},
