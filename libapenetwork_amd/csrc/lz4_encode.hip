@@ -221,8 +221,14 @@ __device__ __forceinline__ uint32_t back4(uint32_t x0, uint32_t y0) {
     return umin(ffbh(x0 ^ y0) >> 3, 4u);
 }
 
+// e / 255 with one full-rate 24-bit multiply: 255 * 0x8081 = 2^23 + 127, so
+// floor(e * 0x8081 / 2^23) = floor(e / 255) for e < 66060 (lengths here are < 65537)
+__device__ __forceinline__ uint32_t div255(uint32_t e) {
+    return (uint32_t)__umul24(e, 0x8081u) >> 23;
+}
+
 __device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {  // bytes after a 15 nibble
-    return v >= 15 ? (v - 15) / 255 + 1 : 0;
+    return v >= 15 ? div255(v - 15) + 1 : 0;
 }
 
 // write the length extension of v (>= 15) at o
@@ -717,30 +723,22 @@ __device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int la
         const uint32_t own = umax(wave_incl_max(mk), carry) - 1u;
         const uint4 r = S.rec[own];
         const uint32_t b = w + (uint32_t)lane;
-        if (b < tot) {
-            const uint32_t rr = b - r.x;                 // offset inside the sequence
-            const uint32_t rl = r.z, rml = r.w & 0xFFFFu, roff = r.w >> 16;
-            const uint32_t lit_at = 1u + ext_bytes(rl), off_at = lit_at + rl;
-            uint32_t v;
-            if (rr == 0u) {
-                v = ((rl < 15u ? rl : 15u) << 4) | (rml < 15u ? rml : 15u);
-            } else if (rr < lit_at) {                    // literal-length extension
-                const uint32_t e = rl - 15u, full = e / 255u;
-                v = (rr - 1u < full) ? 255u : e - 255u * full;
-            } else if (rr < off_at) {                    // literal byte
-                const uint32_t a = r.y + (rr - lit_at);
-                v = a >= rlo ? (uint32_t)((const uint8_t *)S.ring)[a & (kRingE - 1)]
-                             : (uint32_t)B.in[a];
-            } else if (rr == off_at) {
-                v = roff & 0xFFu;
-            } else if (rr == off_at + 1u) {
-                v = roff >> 8;
-            } else {                                     // match-length extension
-                const uint32_t e = rml - 15u, full = e / 255u;
-                v = (rr - off_at - 2u < full) ? 255u : e - 255u * full;
-            }
-            out[b] = (uint8_t)v;
-        }
+        // every candidate value computed, then selected (no divergent branches)
+        const uint32_t rr = b - r.x;                     // offset inside the sequence
+        const uint32_t rl = r.z, rml = r.w & 0xFFFFu, roff = r.w >> 16;
+        const uint32_t el = rl - 15u, fl = div255(el);   // literal-length extension
+        const uint32_t lit_at = 1u + (rl >= 15u ? fl + 1u : 0u), off_at = lit_at + rl;
+        const uint32_t em = rml - 15u, fm = div255(em);  // match-length extension
+        const uint32_t a = r.y + (rr - lit_at);          // literal source position
+        uint32_t v = ((const uint8_t *)S.ring)[a & (kRingE - 1)];
+        if (rr >= lit_at && rr < off_at && a < rlo) v = B.in[a];   // older than the ring (rare)
+        const uint32_t vl = (rr - 1u < fl) ? 255u : el - 255u * fl;
+        const uint32_t vm = (rr - off_at - 2u < fm) ? 255u : em - 255u * fm;
+        const uint32_t vo = rr == off_at ? (roff & 0xFFu) : (roff >> 8);
+        v = rr < off_at ? v : (rr < off_at + 2u ? vo : vm);
+        v = rr < lit_at ? vl : v;
+        v = rr == 0u ? ((umin(rl, 15u) << 4) | umin(rml, 15u)) : v;
+        if (b < tot) out[b] = (uint8_t)v;
     }
     C.o += tot;
 }
