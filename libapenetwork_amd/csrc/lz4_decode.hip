@@ -43,6 +43,7 @@ constexpr int kWinNeed = 84;     // a parse window reads up to P + 63 + 21
 constexpr int kStep = 256;       // output bytes per copy step (4 per lane)
 constexpr int kMaxDesc = 64;     // descriptors per batch
 constexpr int kFlushAt = 40;     // copy once a batch holds more than this (window adds <= 22)
+constexpr int kMaxCarry = 24;    // descriptors carried into the next batch (< kFlushAt)
 
 struct __attribute__((aligned(16))) WaveLds {
     uint8_t ring[kRing];
@@ -198,9 +199,9 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const int p = P + lane;
     const int ipl = p + 1;                       // first literal byte
     const int ipo = ipl + (int)lit + 2;          // after the offset
-    const bool fin_in = (int64_t)ipl + lit > (int64_t)D.csize - 8;
+    const bool fin_in = (uint32_t)ipl + lit + 8u > (uint32_t)D.csize;   // ipl >= 1, csize > 0
     const bool mlx = mn == 15u;
-    const bool mlerr = mlx && ipo > D.csize - kLastLiterals;
+    const bool mlerr = mlx && ipo + kLastLiterals > D.csize;
     const bool cx = lit == 15u || (mlx && e == 255u && !mlerr);
     const uint32_t ml = mlx ? 15u + e : mn;
     const int q = ipo + (mlx ? 1 : 0);           // next token
@@ -225,25 +226,20 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const uint32_t ob = mem ? (fin_in ? lit : lit + ml + kMinMatch) : 0u;
     const uint32_t ex = wave_excl_scan(ob);
     const uint32_t opl = op + ex;
-    const int64_t cpy = (int64_t)opl + lit;
-    const bool fin = fin_in || (PARTIAL ? (cpy > D.oexit) : (cpy > (int64_t)D.cap - kMFLimit));
-    bool stop = false, bad = false;
-    int rv = 0;
-    if (fin) {
-        bad = PARTIAL ? (cpy > D.cap || (int64_t)ipl + lit > D.csize)
-                      : ((int64_t)ipl + lit != D.csize || cpy > D.cap);
-        stop = true;
-        rv = bad ? -ipl - 1 : (int)cpy;
-    } else if (cpy < (int64_t)off) {
-        stop = bad = true;
-        rv = -ipo - 1;
-    } else if (mlerr) {
-        stop = bad = true;
-        rv = -ipo - 1;
-    } else if (cpy + ml + kMinMatch > (int64_t)D.cap - kLastLiterals) {
-        stop = bad = true;
-        rv = -q - 1;
-    }
+    // The checks of :1345-1447 in the reference's order, as selects (no divergent
+    // branches).  32-bit unsigned arithmetic is exact here: cap, csize > 0, a window
+    // token has lit < 15 and ml < 274, and op + ex stays far below 2^32.
+    const uint32_t cpy = opl + lit, ucap = (uint32_t)D.cap;
+    const uint32_t iend = (uint32_t)ipl + lit;  // input position after the literals
+    const bool fin = fin_in || (PARTIAL ? ((int64_t)cpy > D.oexit) : (cpy + (uint32_t)kMFLimit > ucap));
+    const bool badfin = PARTIAL ? (cpy > ucap || iend > (uint32_t)D.csize)
+                                : (iend != (uint32_t)D.csize || cpy > ucap);
+    const bool e_off = cpy < off;                                       // :1375-1376
+    const bool e_cap = cpy + ml + (uint32_t)(kMinMatch + kLastLiterals) > ucap;   // :1444
+    const bool stop = fin || e_off || mlerr || e_cap;
+    const bool bad = fin ? badfin : stop;
+    const int rv = fin ? (badfin ? -ipl - 1 : (int)cpy)
+                       : ((e_off || mlerr) ? -ipo - 1 : -q - 1);
     const uint64_t sm = __ballot(mem && stop) & M;
     uint64_t emit = M;
     int st = ST_MORE;
@@ -319,22 +315,32 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
     bool anyg = false;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
+        // Every arm is computed into a variable first and the ternaries only pick
+        // between plain values: the compiler then emits v_cndmask selects, not the
+        // divergent branches (exec-mask juggling on the scalar unit) that nested
+        // ternaries with arithmetic in their arms become.
         const uint32_t q = q0 + j;
         const bool inB = q >= outB;
-        const uint32_t le = inB ? leB : leA, off = inB ? offB : offA;
+        const uint32_t le = inB ? leB : leA, off = inB ? offB : offA, xl = inB ? xlB : xlA;
         const bool lit = q < le;
-        const uint32_t mb = inB ? q - leB : (q0 >= leA ? rA + j : q - leA);
+        const uint32_t mbB = q - leB, mbA0 = rA + j, mbA1 = q - leA;
+        const uint32_t mbA = q0 >= leA ? mbA0 : mbA1;
+        const uint32_t mb = inB ? mbB : mbA;
         const uint32_t mpos = le - off + reduce3(mb, off);
-        const uint32_t ps = lit ? q + (inB ? xlB : xlA) : mpos;
+        const uint32_t lpos = q + xl;
+        const uint32_t ps = lit ? lpos : mpos;
         const bool live = q >= lo && q < hi && (lit || off != 0u);  // offset 0 -> 0 (App. B)
         const bool inst = ps - s0 < (uint32_t)kStage;
         const bool ring = !lit && ps >= gdone && ps < lo;
         const bool pend = live && !lit && ps >= lo;
+        const uint32_t a_st = ps - s0 + (uint32_t)offsetof(WaveLds, stage), a_rg = ps & (kRing - 1);
+        const uint32_t a_lit = inst ? a_st : 0xFFFFFFFFu, a_mat = ring ? a_rg : 0xFFFFFFFFu;
+        const uint32_t a_live = lit ? a_lit : a_mat;
         pos[j] = ps;
-        lad[j] = !live ? 0xFFFFFFFFu
-                       : (lit ? (inst ? ps - s0 + (uint32_t)offsetof(WaveLds, stage) : 0xFFFFFFFFu)
-                              : (ring ? (ps & (kRing - 1)) : 0xFFFFFFFFu));
-        gk[j] = !live || pend ? 0u : (lit ? (inst ? 0u : 1u) : (ps < gdone ? 2u : 0u));
+        lad[j] = live ? a_live : 0xFFFFFFFFu;
+        const uint32_t g_lit = inst ? 0u : 1u, g_mat = ps < gdone ? 2u : 0u;
+        const uint32_t g_live = lit ? g_lit : g_mat;
+        gk[j] = (live && !pend) ? g_live : 0u;
         anyg |= gk[j] != 0u;
         pendm |= pend ? 1u << j : 0u;
     }
@@ -473,10 +479,14 @@ lz4_decode_kernel(BlockArgs a) {
     stage_load(L, D.src, D.csize, D.s0, lane);
     wave_sync();
 
+    // Output is copied in whole 256-byte steps: a batch copies up to the last step
+    // boundary its sequences reach and carries the descriptors of the unfinished
+    // step into the next batch (the last batch copies everything), so each step is
+    // produced once instead of once per batch that touches it.
+    uint32_t cstart = 0;     // output [0, cstart) copied
+    int nd = 0;              // descriptors in L.desc (carried ones first)
     while (st == ST_MORE) {
         // ---- PARSE one batch ----
-        const uint32_t bstart = op;
-        int nd = 0;
         bool restage = false;
         while (st == ST_MORE && nd <= kFlushAt) {
             if (P - D.s0 + kWinNeed > kStage) { restage = true; break; }
@@ -490,17 +500,26 @@ lz4_decode_kernel(BlockArgs a) {
         }
         STAT(0);
         if (st == ST_ERR) break;
-        // ---- COPY the batch's output [bstart, op) ----
+        // ---- COPY the batch's output [cstart, cend) ----
         wave_sync();
         const uint32_t bend = op;
         const uint32_t d_out = lane < nd ? L.desc[lane].y : 0u;
+        // Copy through the last step boundary and carry the descriptors from the
+        // owner of that boundary on; with no new boundary, carry them all.  The
+        // last batch, or one that would carry too many, copies through its end.
+        uint32_t cend = bend & ~(uint32_t)(kStep - 1);
+        int keep = 0;
+        if (cend > cstart) keep = __popcll(__ballot(lane < nd && d_out <= cend)) - 1;
+        else cend = cstart;
+        const bool carry = st == ST_MORE && cend < bend && nd - keep <= kMaxCarry;
+        if (!carry) cend = bend;
 #ifdef APE_DEXP_NOCOPY
-        for (uint32_t base = bend; base < bend; base += kStep) {
+        for (uint32_t base = cend; base < cend; base += kStep) {
 #else
-        for (uint32_t base = bstart & ~(uint32_t)(kStep - 1); base < bend; base += kStep) {
+        for (uint32_t base = cstart & ~(uint32_t)(kStep - 1); base < cend; base += kStep) {
 #endif
-            const uint32_t lo = base > bstart ? base : bstart;
-            const uint32_t hi = base + kStep < bend ? base + kStep : bend;
+            const uint32_t lo = base > cstart ? base : cstart;
+            const uint32_t hi = base + kStep < cend ? base + kStep : cend;
             if (lo - gdone > (uint32_t)(kRing / 2)) {
                 __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 gdone = lo;
@@ -508,6 +527,16 @@ lz4_decode_kernel(BlockArgs a) {
             wave_sync();
             copy_step(L, D, base, lo, hi, gdone, nd, d_out);
             STAT_ADD(3, 1);
+        }
+        cstart = cend;
+        if (carry) {   // desc[keep, nd) -> desc[0, nd - keep)
+            wave_sync();
+            const uint4 dv = L.desc[keep + (lane < nd - keep ? lane : 0)];
+            wave_sync();
+            if (lane < nd - keep) L.desc[lane] = dv;
+            nd -= keep;
+        } else {
+            nd = 0;
         }
         STAT(1);
         STAT_ADD(2, 1);
