@@ -65,7 +65,7 @@ constexpr uint32_t kEagerLen = 28;   // match bytes measured by the producer
 #endif
 constexpr uint32_t kRingE = APE_LZ4_ERING;  // recent input bytes (own, stage 2, end-2, literals)
 #ifndef APE_LZ4_SCRBITS
-#define APE_LZ4_SCRBITS 7
+#define APE_LZ4_SCRBITS 6
 #endif
 constexpr uint32_t kScr = 1u << APE_LZ4_SCRBITS;  // in-chunk candidate scratch entries
 constexpr int kSmall = 128;          // smaller blocks take the byte-load path
@@ -82,10 +82,12 @@ struct __attribute__((aligned(16))) EncLds {
     // input byte x at ring byte (x mod kRingE); the first 64 bytes are mirrored
     // after the end, so a 36-byte read never wraps (immediate LDS offsets)
     uint32_t ring[kRingE / 4 + 16];
-    uint2 info[2][64];
+    uint2 info[3][64];               // producer -> walker and emitter, chunk k in [k % 3]
     uint32_t scr[kScr];              // producer scratch: earliest lane per low hash bits
-    uint4 rec[64];                   // consumer: sequence records of the chunk being emitted
-    uint32_t omap[16];               // consumer: owner map of a 64-byte output window
+    uint2 wres[2][64];               // walker -> emitter: {m_len | m_back << 20, anchor}
+    uint32_t wmem[2][2];             // walker -> emitter: member mask of the chunk
+    uint32_t wend;                   // walker -> emitter: final anchor (last literals)
+    uint32_t omap[16];               // emitter: owner map of a 64-byte output window
 };
 
 // s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt at their maxima = no wait).  The
@@ -410,20 +412,15 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
         const uint32_t at = p + len - 2u;         // match end - 2 (:680)
         if (at + 5u <= B.un) e2 = I_E2 | (hash5(ring4(S, at), ring4(S, at + 4u)) << 16);
     }
-    S.info[k & 1][lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
+    S.info[k % 3][lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
                                          (R.has ? I_HAS : 0u) | (R.hashable ? I_HASHABLE : 0u) | e2,
                                      (R.has ? p - R.c : 0u) | (R.h << 16));
 }
 
-// ---------------- consumer ----------------
-struct Cons {
+// ---------------- walker ----------------
+struct Walk {
     uint32_t q;          // walk position
     uint32_t anchor;     // start of the pending literals
-    uint32_t o;          // output cursor
-    bool overflow;
-    uint64_t walked, members;
-    uint32_t m_back, m_len, anchor0;  // per member lane / at the step start
-    uint32_t an;         // per member lane: end of the previous member (or anchor0)
 };
 
 // forward extension of the match at m (candidate cm) from L bytes on, with the
@@ -467,148 +464,32 @@ __device__ __forceinline__ uint32_t extend_match(const Blk &B, uint32_t m, uint3
     return L > lm ? lm : L;
 }
 
-#ifdef APE_DBG_WALK
-__device__ int g_dbg_count;
-// the serial walk (debug reference for the parallel one)
-__device__ __forceinline__ void cons_walk_ref(const EncLds &S, const Blk &B, int k, int lane, Cons &C) {
-    const uint32_t P = 64u * (uint32_t)k;
-    C.walked = 0;
-    C.members = 0;
-    C.anchor0 = C.anchor;
-#ifdef APE_EXP_NO_WALK
-    return;
-#endif
-    if (C.overflow || C.q >= P + 64u) return;
-    const uint2 iv = S.info[k & 1][lane];
-    const uint64_t Mm = __ballot((iv.x & I_HAS) != 0u);
-    uint32_t q = C.q;
-    for (;;) {
-        const uint32_t rel = q - P;
-        if (rel >= 64u) break;
-        const uint64_t w = Mm >> rel;
-        if (w == 0) {
-            C.walked |= ~0ull << rel;
-            q = P + 64u;
-            break;
-        }
-        const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
-        C.walked |= (~0ull << rel) & (j == 63 ? ~0ull : ((2ull << j) - 1ull));
-        const uint32_t v = lane_val(iv.x, (int)j);
-        const uint32_t m = P + j;
-        uint32_t L = v & 0xFFu;
-        if (v & I_TRUNC) {
-            // forward extension with the whole wave, 1 KiB per step
-            const uint32_t cm = m - (lane_val(iv.y, (int)j) & 0xFFFFu);
-            const uint32_t lm = B.mlimit - m;
-            for (;;) {
-                const uint32_t kk = L + 16u * (uint32_t)lane;
-                uint32_t d = 0, at = 0;
-                if (kk < lm) {
-                    uint32_t xb[4] = {0, 0, 0, 0}, yb[4] = {0, 0, 0, 0};
-                    if (m + kk + 16u <= B.un) {
-                        const uint4 x = gload16(B.in + (m + kk)), y = gload16(B.in + (cm + kk));
-                        xb[0] = x.x; xb[1] = x.y; xb[2] = x.z; xb[3] = x.w;
-                        yb[0] = y.x; yb[1] = y.y; yb[2] = y.z; yb[3] = y.w;
-                    } else {
-#pragma unroll
-                        for (uint32_t t = 0; t < 16u; t++) {
-                            if (m + kk + t < B.un) {
-                                xb[t >> 2] |= (uint32_t)B.in[m + kk + t] << (8 * (t & 3));
-                                yb[t >> 2] |= (uint32_t)B.in[cm + kk + t] << (8 * (t & 3));
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int t = 3; t >= 0; t--) {
-                        const uint32_t e = xb[t] ^ yb[t];
-                        if (e) { d = 1; at = 4u * (uint32_t)t + (__builtin_ctz(e) >> 3); }
-                    }
-                }
-                const uint64_t bad = __ballot(d != 0 || kk >= lm);
-                if (bad) {
-                    const int fl = __builtin_ctzll(bad);
-                    const uint32_t k2 = L + 16u * (uint32_t)fl;
-                    L = k2 >= lm ? lm : k2 + lane_val(at, fl);
-                    break;
-                }
-                L += 1024u;
-            }
-            if (L > lm) L = lm;
-        }
-        uint32_t bkj = (v >> 8) & 7u;
-        if (bkj > m - C.anchor) bkj = m - C.anchor;   // never back into emitted bytes
-        if (lane == (int)j) { C.m_back = bkj; C.m_len = L + bkj; }
-        C.members |= 1ull << j;
-        q = m + L;
-        C.anchor = q;
-    }
-    C.q = q;
-}
-#endif
-
-// first half: walk chunk k (no table writes).
+// Walk chunk k (first half of step k + 1), then (second half) insert the walked
+// positions and match_end - 2 into the table and hand the members to the emitter.
 // The greedy chain (:591-627: a position with a match jumps past it, any other
-// position is a literal).  The scalar unit hops over the match lanes only (ballot
-// mask, one v_readlane per member); everything else -- walked positions, catch-up
-// limits, the new anchor -- follows for all 64 lanes at once from the member set.
-// A match the producer could not finish (TRUNC) is extended with the whole wave.
-// APE_WALK_DOUBLING selects a variant that resolves the chain by pointer doubling
-// (ds_permute / ds_bpermute, six rounds): no scalar loop, but six LDS round trips.
-__device__ __forceinline__ void cons_walk(const EncLds &S, const Blk &B, int k, int lane, Cons &C) {
+// position is a literal): the scalar unit hops over the match lanes only (ballot
+// mask, one v_readlane per member); walked positions, catch-up limits (:623-627)
+// and the new anchor follow for all 64 lanes at once from the member set.  A match
+// the producer could not finish (TRUNC, >= 60 bytes) is extended by the whole wave.
+struct WalkOut {
+    uint64_t walked, members;
+    uint32_t m_back, m_len, an;   // per member lane
+    uint2 iv;
+};
+
+__device__ __forceinline__ void walk_chunk(const EncLds &S, const Blk &B, int k, int lane, Walk &W,
+                                           WalkOut &O) {
     const uint32_t P = 64u * (uint32_t)k;
-    C.walked = 0;
-    C.members = 0;
-    C.anchor0 = C.anchor;
-#ifdef APE_EXP_NO_WALK
-    return;
-#endif
-    if (C.overflow || C.q >= P + 64u) return;
-#ifdef APE_DBG_WALK
-    Cons R = C;
-    cons_walk_ref(S, B, k, lane, R);
-    const uint32_t q0dbg = C.q;
-#endif
-    const uint2 iv = S.info[k & 1][lane];
+    O.walked = O.members = 0;
+    O.m_back = O.m_len = O.an = 0;
+    O.iv = S.info[k % 3][lane];
+    if (W.q >= P + 64u) return;               // a match from earlier chunks covers it
+    const uint2 iv = O.iv;
     const bool has = (iv.x & I_HAS) != 0u, trunc = (iv.x & I_TRUNC) != 0u;
     uint32_t Lf = iv.x & 0xFFu;                          // forward match length
-    uint32_t q = C.q;
-#ifdef APE_WALK_DOUBLING
-    // one hop: a finished match jumps past its end, a literal to the next position,
-    // an unfinished match leaves the chunk (resolved below)
-    const uint32_t J0 = has ? (trunc ? 64u : umin((uint32_t)lane + Lf, 64u)) : (uint32_t)lane + 1u;
-    for (;;) {
-        const uint32_t rel = q - P;
-        uint32_t J = J0, m = (uint32_t)lane == rel ? 1u : 0u;
-#pragma unroll
-        for (int r = 0; r < 6; r++) {
-            const bool in = J < 64u;
-            // marks that stay in the chunk go to lane J; all other lanes send 0 to lane 0
-            // (no hop lands on 0, and lane 0 keeps its own mark through the OR)
-            const bool go = m && in;
-            const uint32_t t = (uint32_t)__builtin_amdgcn_ds_permute((int)(go ? 4u * J : 0u), go ? 1 : 0);
-            const uint32_t Jn = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (in ? J : 0u)), (int)J);
-            m |= t;
-            J = in ? Jn : J;
-        }
-        C.members |= __ballot(m != 0u && has);
-        const uint64_t ex = __ballot(m != 0u && J0 >= 64u);   // the node that leaves
-        const int e = __builtin_ctzll(ex);
-        const uint32_t ve = lane_val(iv.x, e);
-        if (!(ve & I_TRUNC)) {            // a finished match, or the literal at 63
-            q = P + (uint32_t)e + ((ve & I_HAS) ? (ve & 0xFFu) : 1u);
-            break;
-        }
-        const uint32_t me = P + (uint32_t)e;
-        const uint32_t cm = me - (lane_val(iv.y, e) & 0xFFFFu);
-        const uint32_t Le = extend_match(B, me, cm, ve & 0xFFu, lane);
-        if (lane == e) Lf = Le;
-        q = me + Le;
-        if (q >= P + 64u) break;
-    }
-#else
     const uint64_t Hm = __ballot(has);
     const uint32_t Lh = has ? (trunc ? 0x80u : Lf) : 0u;   // hop; 0x80 = unfinished
-    uint32_t rel = q - P;
+    uint32_t rel = W.q - P;
     uint64_t M = 0;
     for (;;) {
         const uint64_t w = Hm >> rel;
@@ -627,50 +508,32 @@ __device__ __forceinline__ void cons_walk(const EncLds &S, const Blk &B, int k, 
         }
         if (rel >= 64u) break;
     }
-    q = P + rel;
-    C.members = M;
-#endif
     // catch-up limits: a member's backward extension stops at the previous end
-    const bool mem = (C.members >> lane) & 1ull;
+    const uint32_t anchor0 = W.anchor;
+    const bool mem = (M >> lane) & 1ull;
     const uint32_t p = P + (uint32_t)lane;
     const uint32_t end = mem ? p + Lf : 0u;
     const uint32_t imax = wave_incl_max(end);
-    const uint32_t pm = umax(wave_shr1(imax, 0u), C.anchor0);
+    const uint32_t pm = umax(wave_shr1(imax, 0u), anchor0);
     const uint32_t bk = umin((iv.x >> 8) & 7u, p - pm);
-    C.m_back = bk;
-    C.m_len = Lf + bk;
-    C.an = pm;
-    C.anchor = umax(C.anchor0, lane_val(imax, 63));
+    O.members = M;
+    O.m_back = bk;
+    O.m_len = Lf + bk;
+    O.an = pm;
     // walked = every position from the walk start that no match of this chunk covers
-    C.walked = __ballot(p >= C.q && pm <= p);
-    C.q = q;
-#ifdef APE_DBG_WALK
-    {
-        const bool bad = R.walked != C.walked || R.members != C.members || R.q != C.q ||
-                         R.anchor != C.anchor ||
-                         __ballot(mem && (R.m_back != C.m_back || R.m_len != C.m_len)) != 0;
-        if (bad && lane == 0 && atomicAdd(&g_dbg_count, 1) < 8)
-            printf("walk k=%d q0=%u: W %llx/%llx M %llx/%llx q %u/%u anc %u/%u\n", k, q0dbg,
-                   (unsigned long long)R.walked, (unsigned long long)C.walked,
-                   (unsigned long long)R.members, (unsigned long long)C.members, R.q, C.q,
-                   R.anchor, C.anchor);
-    }
-#endif
+    O.walked = __ballot(p >= W.q && pm <= p);
+    W.anchor = umax(anchor0, lane_val(imax, 63));
+    W.q = P + rel;
 }
 
-// second half: table updates, then emission of chunk k's sequences
-__device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int lane, Cons &C) {
-    if (C.overflow) return;
-    const uint32_t P = 64u * (uint32_t)k;
-    const uint32_t p = P + (uint32_t)lane;
-    const uint2 iv = S.info[k & 1][lane];
-    if (((C.walked >> lane) & 1ull) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
-    const bool mem = (C.members >> lane) & 1ull;
-    // during this half the producer has written chunks up to k + 3, so the ring
-    // holds input [rlo, P + 256)
-    const uint32_t rlo = P + 256u > kRingE ? P + 256u - kRingE : 0u;
-    const uint32_t fwd = C.m_len - C.m_back;     // match length from p
-    // match_end - 2: hashed by the producer unless the consumer extended the match
+__device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int lane,
+                                             const WalkOut &O) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const uint2 iv = O.iv;
+    if (((O.walked >> lane) & 1ull) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
+    const bool mem = (O.members >> lane) & 1ull;
+    const uint32_t fwd = O.m_len - O.m_back;      // match length from p
+    // match_end - 2 (:680): hashed by the producer unless the walker extended the match
     uint32_t e2h = (iv.x >> 16) & (kHSize - 1);
     bool e2ok = mem && (iv.x & I_E2) && !(iv.x & I_TRUNC);
     if (mem && (iv.x & I_TRUNC)) {
@@ -685,32 +548,66 @@ __device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int la
             e2ok = true;
         }
     }
-    // LDS operations of one wave complete in order: the walked-position inserts
-    // above land before these (compiler barrier only, no counter wait)
+    // one wave's LDS operations complete in order: the walked-position inserts above
+    // land before these (compiler barrier only)
     __builtin_amdgcn_sched_barrier(0);
     if (e2ok) S.tab[e2h] = (uint16_t)(p + fwd - 2u);
-#ifdef APE_EXP_NO_EMIT
-    C.members = 0;
-#endif
-    if (!C.members) return;
-    const uint32_t ms = p - C.m_back;            // match start after catch-up
-    const uint32_t an = C.an;
-    const uint32_t lit = mem ? ms - an : 0u;
-    const uint32_t ml = C.m_len - kMinMatch;
-    const uint32_t size = mem ? 1u + ext_bytes(lit) + lit + 2u + ext_bytes(ml) : 0u;
-    const uint32_t ex = wave_excl_scan(size);
-    const uint32_t tot = lane_val(ex + size, 63);
-    if ((uint64_t)C.o + tot > B.cap) {
-        C.overflow = true;
-        return;
+    S.wres[k & 1][lane] = make_uint2(O.m_len | (O.m_back << 20), O.an);
+    if (lane == 0) {
+        S.wmem[k & 1][0] = (uint32_t)O.members;
+        S.wmem[k & 1][1] = (uint32_t)(O.members >> 32);
     }
-    // Gather: lane L of window w produces output byte w + L.  Its sequence is the
-    // last member starting at or before it (owner map + prefix max).
-    // (one wave's LDS operations complete in order, so the owner-map writes, the
-    // read-back and the clearing need no counter waits between them; omap is all
-    // zero between windows)
-    if (mem) S.rec[lane] = make_uint4(ex, an, lit, ml | ((iv.y & 0xFFFFu) << 16));
-    gu8 *out = B.dst + C.o;
+}
+
+// ---------------- emitter ----------------
+struct Emit {
+    uint32_t o;          // output cursor
+    bool overflow;
+    // chunk being emitted (set in the first half, used in the second)
+    uint64_t members;
+    uint32_t tot, ex, an, lit, mo;
+};
+
+// First half of step k + 2: sizes and output offsets of chunk k's sequences.
+__device__ __forceinline__ void emit_prepare(const EncLds &S, const Blk &B, int k, int lane, Emit &E) {
+    E.tot = 0;
+    const uint64_t members = ((uint64_t)__builtin_amdgcn_readfirstlane(S.wmem[k & 1][1]) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane(S.wmem[k & 1][0]);
+    E.members = E.overflow ? 0ull : members;
+    if (!E.members) return;
+    const uint2 wr = S.wres[k & 1][lane];
+    const uint32_t off = S.info[k % 3][lane].y & 0xFFFFu;
+    const bool mem = (E.members >> lane) & 1ull;
+    const uint32_t m_len = wr.x & 0xFFFFFu, m_back = wr.x >> 20;
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const uint32_t ms = p - m_back;            // match start after catch-up
+    E.an = wr.y;
+    E.lit = mem ? ms - E.an : 0u;
+    const uint32_t ml = m_len - kMinMatch;
+    const uint32_t size = mem ? 1u + ext_bytes(E.lit) + E.lit + 2u + ext_bytes(ml) : 0u;
+    E.ex = wave_excl_scan(size);
+    E.tot = lane_val(E.ex + size, 63);
+    E.mo = ml | (off << 16);
+    if ((uint64_t)E.o + E.tot > B.cap) {
+        E.overflow = true;
+        E.members = 0;
+        E.tot = 0;
+    }
+}
+
+// Second half of step k + 2: gather.  Lane L of window w produces output byte w + L;
+// its sequence is the last member starting at or before it (owner map + prefix max),
+// whose record comes over by ds_bpermute.  One wave's LDS operations complete in
+// order, so the owner-map writes, the read-back and the clearing need no waits.
+__device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int k, int lane, Emit &E) {
+    if (!E.members) return;
+    const uint32_t P = 64u * (uint32_t)k;
+    // during this half the producer has written chunks up to k + 4, so the ring
+    // holds input [rlo, P + 320)
+    const uint32_t rlo = P + 320u > kRingE ? P + 320u - kRingE : 0u;
+    const bool mem = (E.members >> lane) & 1ull;
+    const uint32_t ex = E.ex, tot = E.tot;
+    gu8 *out = B.dst + E.o;
     for (uint32_t w = 0; w < tot; w += 64u) {
         const bool mark = mem && ex > w && ex < w + 64u;
         if (mark) ((uint8_t *)S.omap)[ex - w] = (uint8_t)(lane + 1);
@@ -720,16 +617,19 @@ __device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int la
         if (mark) ((uint8_t *)S.omap)[ex - w] = 0;
         const uint64_t cov = __ballot(mem && ex <= w);   // member 0 starts at 0
         const uint32_t carry = 64u - (uint32_t)__clzll((long long)cov);
-        const uint32_t own = umax(wave_incl_max(mk), carry) - 1u;
-        const uint4 r = S.rec[own];
+        const int own = (int)(umax(wave_incl_max(mk), carry) - 1u);
+        const uint32_t r_ex = (uint32_t)__builtin_amdgcn_ds_bpermute(own << 2, (int)ex);
+        const uint32_t r_an = (uint32_t)__builtin_amdgcn_ds_bpermute(own << 2, (int)E.an);
+        const uint32_t rl = (uint32_t)__builtin_amdgcn_ds_bpermute(own << 2, (int)E.lit);
+        const uint32_t r_mo = (uint32_t)__builtin_amdgcn_ds_bpermute(own << 2, (int)E.mo);
         const uint32_t b = w + (uint32_t)lane;
         // every candidate value computed, then selected (no divergent branches)
-        const uint32_t rr = b - r.x;                     // offset inside the sequence
-        const uint32_t rl = r.z, rml = r.w & 0xFFFFu, roff = r.w >> 16;
+        const uint32_t rr = b - r_ex;                    // offset inside the sequence
+        const uint32_t rml = r_mo & 0xFFFFu, roff = r_mo >> 16;
         const uint32_t el = rl - 15u, fl = div255(el);   // literal-length extension
         const uint32_t lit_at = 1u + (rl >= 15u ? fl + 1u : 0u), off_at = lit_at + rl;
         const uint32_t em = rml - 15u, fm = div255(em);  // match-length extension
-        const uint32_t a = r.y + (rr - lit_at);          // literal source position
+        const uint32_t a = r_an + (rr - lit_at);         // literal source position
         uint32_t v = ((const uint8_t *)S.ring)[a & (kRingE - 1)];
         if (rr >= lit_at && rr < off_at && a < rlo) v = B.in[a];   // older than the ring (rare)
         const uint32_t vl = (rr - 1u < fl) ? 255u : el - 255u * fl;
@@ -740,53 +640,43 @@ __device__ __forceinline__ void cons_emit(EncLds &S, const Blk &B, int k, int la
         v = rr == 0u ? ((umin(rl, 15u) << 4) | umin(rml, 15u)) : v;
         if (b < tot) out[b] = (uint8_t)v;
     }
-    C.o += tot;
+    E.o += tot;
 }
 
+// ---------------- block ----------------
+// Three waves per block, one role each, in lock step (two barriers per step):
+//   step s, first half : producer A(s+3) B(s+2) C1(s+1) | walker walks s-1 | emitter sizes s-2
+//   step s, second half: producer C2(s) -> info[s%3]     | walker inserts s-1, publishes
+//                                                         | emitter writes s-2
+// Table inserts (second half) never overlap the producer's lookups (first half).
 template <bool SMALL>
 __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, int lane,
                                              int *result) {
     STATS_DECL
-    PSet P0, P1;
-    Cons C;
-    C.q = 0;
-    C.anchor = 0;
-    C.o = 0;
-    C.overflow = false;
-    C.walked = C.members = 0;
-    C.m_back = C.m_len = C.anchor0 = C.an = 0;
     const int nch = B.n >= kMinLength ? B.nch : 0;   // :584, shorter -> last literals only
-    const int nsteps = (nch + 2) & ~1;   // >= nch + 1 producer/consumer steps, even
+    const int nsteps = (nch + 3) & ~1;   // >= nch + 2 steps (emission lags two), even
 
-#ifdef APE_EXP_PRIO_CONS
-    if (wave == 0) __builtin_amdgcn_s_setprio(APE_EXP_PRIO_CONS);
-#endif
-#ifdef APE_EXP_PRIO_PROD
-    if (wave == 1) __builtin_amdgcn_s_setprio(APE_EXP_PRIO_PROD);
-#endif
-    // The two roles run separate loops (same number of barriers: 1 + 2 per step), so
-    // the compiler's memory-counter waits in each loop see only that role's loads
-    // and stores -- a shared loop merges both roles' in-flight operations at every
-    // join and turns the producer's pipelined waits into full ones.
+    // Each role runs its own loop (same barrier count: 1 + 2 per step), so the
+    // compiler's memory-counter waits in each loop see only that role's operations.
     if (wave == 1) {
+        PSet P0, P1;
         // one producer step; `cur` = set of parity s, `nxt` = parity s + 1
         auto pstep = [&](auto fast, int s, PSet &cur, PSet &nxt) {
             constexpr bool F = decltype(fast)::value;
-            // first half: A(s+3), B(s+2).  In flight, oldest first: A(s+2), Y(s+1) x2,
-            // E(s) x2 -> A(s+2) has landed once at most 4 remain.
             // Every stage runs on every step, past the last chunk too (it then loads
             // from the block start and records nothing), so the number of loads per
             // step -- and with it the waits -- is the same on every path.
+            // In flight, oldest first: A(s+2), Y(s+1) x2, E(s) x2 -> A(s+2) at 4.
             vm_wait<4>();
             prod_load<SMALL, F>(B, s + 3, lane, nxt.X);
             prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
+            // Y(s+1) x2, E(s) x2, A(s+3), Y(s+2) x2 -> Y(s+1) at 5
+            vm_wait<5>();
+            prod_measure<SMALL, F>(S, B, s + 1, lane, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q, nxt.E);
             STAT(5);
             __syncthreads();
             STAT(6);
-            // second half: C1(s+1), C2(s).  In flight: Y(s+1) x2, E(s) x2, A(s+3),
-            // Y(s+2) x2 -> Y(s+1) at 5; after C1 issues E(s+1) x2, E(s) at 5.
-            vm_wait<5>();
-            prod_measure<SMALL, F>(S, B, s + 1, lane, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q, nxt.E);
+            // E(s) x2, A(s+3), Y(s+2) x2, E(s+1) x2 -> E(s) at 5
             vm_wait<5>();
             prod_finish(S, B, s, lane, cur.q, cur.E);
             STAT(7);
@@ -801,11 +691,9 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             prod_lookup<SMALL>(S, B, 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
             prod_measure<SMALL>(S, B, 0, lane, P0.Y, P0.cT, P0.jL, P0.h, P0.q, P0.E);
         }
-#ifndef APE_EXP_NO_PROLOGUE_WAIT
         // nothing in flight at the loop entry, so the loop's counter waits depend only
         // on its own issue order (once per block)
         __builtin_amdgcn_s_waitcnt(0);
-#endif
         __syncthreads();
         // Steps whose three loads all lie inside the block (A(s+3): 64(s+3)+72 <= n,
         // Y(s+2): 64(s+2)+91, E(s+1): 64(s+1)+123) run a loop without the edge paths;
@@ -824,48 +712,74 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         STATS_FLUSH_TID(g_enc_stats, 64);
         return;
     }
-    // consumer: walk / table + emission of chunk s-1 during producer step s
+    if (wave == 0) {   // walker: chunk s-1 during step s
+        Walk W;
+        W.q = 0;
+        W.anchor = 0;
+        WalkOut O;
+        __syncthreads();
+        for (int s = 0; s < nsteps; s++) {
+            const bool work = s >= 1 && s <= nch;
+            if (work) walk_chunk(S, B, s - 1, lane, W, O);
+            STAT(0);
+            __syncthreads();
+            STAT(4);
+            if (work) {
+                walk_publish(S, B, s - 1, lane, O);
+                STAT_ADD(11, __popcll(O.members));
+            }
+            if (s == nsteps - 1 && lane == 0) S.wend = W.anchor;
+            STAT(1);
+            STAT_ADD(10, 3);
+            __syncthreads();
+            STAT(3);
+        }
+        STATS_FLUSH(g_enc_stats);
+        return;
+    }
+    // emitter: chunk s-2 during step s
+    Emit E;
+    E.o = 0;
+    E.overflow = false;
+    E.members = 0;
+    E.tot = E.ex = E.an = E.lit = E.mo = 0;
     __syncthreads();
     for (int s = 0; s < nsteps; s++) {
-        const bool work = s >= 1 && s <= nch;
-        if (work) cons_walk(S, B, s - 1, lane, C);
-        STAT(0);
+        const bool work = s >= 2 && s <= nch + 1;
+        if (work) emit_prepare(S, B, s - 2, lane, E);
+        STAT(12);
         __syncthreads();
-        STAT(4);
-        if (work) {
-            cons_emit(S, B, s - 1, lane, C);
-            STAT_ADD(11, __popcll(C.members));
-        }
-        STAT(1);
-        STAT_ADD(10, 2);
+        STAT(14);
+        if (work) emit_write(S, B, s - 2, lane, E);
+        STAT(2);
         __syncthreads();
-        STAT(3);
+        STAT(15);
     }
-    // ---- last literals (:732-751) ----
-    if (!C.overflow) {
-        const uint32_t lit = B.un - C.anchor;
+    // ---- last literals (:732-751), from the walker's final anchor ----
+    if (!E.overflow) {
+        const uint32_t anchor = S.wend;
+        const uint32_t lit = B.un - anchor;
         const uint32_t hdr = 1u + ext_bytes(lit);
-        const uint32_t total = C.o + hdr + lit;
+        const uint32_t total = E.o + hdr + lit;
         if (total > B.cap) {
-            C.overflow = true;
+            E.overflow = true;
         } else {
             if (lane == 0) {
-                B.dst[C.o] = (uint8_t)((lit < 15u ? lit : 15u) << 4);
-                put_len(B.dst + C.o + 1, lit);
+                B.dst[E.o] = (uint8_t)((lit < 15u ? lit : 15u) << 4);
+                put_len(B.dst + E.o + 1, lit);
             }
-            wave_copy(B.in, B.dst, C.anchor, C.o + hdr, lit, lane);
-            C.o = total;
+            wave_copy(B.in, B.dst, anchor, E.o + hdr, lit, lane);
+            E.o = total;
         }
     }
-    if (lane == 0) *result = C.overflow ? 0 : (int)C.o;
-    STAT(2);
+    if (lane == 0) *result = E.overflow ? 0 : (int)E.o;
     STAT_ADD(13, 1);
-    STATS_FLUSH(g_enc_stats);
+    STATS_FLUSH_TID(g_enc_stats, 128);
 }
 
 }  // namespace
 
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(6)))
 lz4_encode_kernel(BlockArgs a) {
     __shared__ EncLds S;
     const int b = blockIdx.x;
@@ -890,9 +804,9 @@ lz4_encode_kernel(BlockArgs a) {
     B.nch = (B.n + 63) / 64;
 
     // table = 0 (the reference's memset state: position 0 for every hash)
-    for (int i = tid; i < kHSize / 8; i += 128) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
-    for (int i = tid; i < (int)kScr; i += 128) S.scr[i] = 0xFFFFFFFFu;
-    for (int i = tid; i < (int)(kRingE / 16 + 4); i += 128) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < kHSize / 8; i += 192) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < (int)kScr; i += 192) S.scr[i] = 0xFFFFFFFFu;
+    for (int i = tid; i < (int)(kRingE / 16 + 4); i += 192) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
     if (tid < 16) S.omap[tid] = 0u;
     __syncthreads();
     if (B.n < kSmall) encode_block<true>(S, B, wave, lane, &a.result[b]);
@@ -901,7 +815,7 @@ lz4_encode_kernel(BlockArgs a) {
 
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(lz4_encode_kernel, dim3(a.nblocks), dim3(128), 0, s, a);
+    hipLaunchKernelGGL(lz4_encode_kernel, dim3(a.nblocks), dim3(192), 0, s, a);
     return hipGetLastError();
 }
 

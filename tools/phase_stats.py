@@ -15,9 +15,9 @@ sys.path.insert(0, ROOT)
 
 DEC = ["parse", "copy", "(batches)", "(steps)", "(restages)", "", "", "", "", "", "(blocks)", "", "", "",
        "", ""]
-ENC = ["C walk", "C table+emit", "C last", "C wait end", "C wait mid", "P load+lookup",
-       "P wait mid", "P measure+finish", "P wait end", "", "(steps x2 waves)", "(members)", "",
-       "(blocks)", "", ""]
+ENC = ["W walk", "W publish", "E write", "W wait end", "W wait mid", "P A+B+C1",
+       "P wait mid", "P C2", "P wait end", "", "(steps x3 waves)", "(members)", "E prepare",
+       "(blocks)", "E wait mid", "E wait end"]
 
 
 def main():
