@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Summarise tools/pmc_traffic.sh: HBM bytes per block and per launch of each codec kernel
+-> profiles/pmc_traffic.json (read by bench.py for roofline.traffic)."""
+import csv
+import glob
+import json
+import shutil
+import sys
+
+nb = int(sys.argv[1])
+out = {"_note": ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
+                 "`bench.py --blocks %d --steps 1 --warmup 0` (input %.1f GiB, past the 256 MiB "
+                 "Infinity Cache); FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 tallies "
+                 "128-B requests at 64 B), KB -> bytes, per launch / blocks.  Raw: "
+                 "profiles/r1_pmc_fetch_size.csv, profiles/r1_pmc_write_size.csv"
+                 % (nb, nb * 65536 / 2**30)),
+       "blocks": nb}
+vals = {}
+for c, dst in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+    files = glob.glob("gpurun_out/pmc_%s/*counter_collection.csv" % c) + \
+        glob.glob("gpurun_out/pmc_%s/*/*counter_collection.csv" % c)
+    shutil.copy(files[0], "profiles/r1_pmc_%s.csv" % c.lower())
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"]
+            name = ("lz4_encode_kernel" if "encode" in k else
+                    "lz4_decode_kernel" if "decode" in k else None)
+            if name and r["Counter_Name"] == c:
+                vals.setdefault(name, {}).setdefault(dst, []).append(float(r["Counter_Value"]))
+for name, d in vals.items():
+    fetch = sum(d.get("fetch", [0])) / max(len(d.get("fetch", [1])), 1) * 1024 * 2
+    write = sum(d.get("write", [0])) / max(len(d.get("write", [1])), 1) * 1024
+    out[name] = {"fetch_bytes_per_block": round(fetch / nb, 1),
+                 "write_bytes_per_block": round(write / nb, 1),
+                 "bytes_per_block": round((fetch + write) / nb, 1)}
+json.dump(out, open("profiles/pmc_traffic.json", "w"), indent=1)
+print(json.dumps(out, indent=1))
