@@ -333,12 +333,17 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
     const bool hashable = live && p + 5u <= B.un;
     h = hash5(X[0], X[1]);
     cT = S.tab[h];
+#ifdef APE_EXP_NO_L
+    jL = 0xFFFFFFFFu;
+    (void)hashable;
+#else
     const uint32_t hs = h & (kScr - 1u);
     if (hashable) atomicMin(&S.scr[hs], (uint32_t)lane);
     wave_sync();
     jL = hashable ? S.scr[hs] : 0xFFFFFFFFu;
     wave_sync();
     if (hashable) S.scr[hs] = 0xFFFFFFFFu;
+#endif
     // ring copy of this chunk (own bytes for C1, second stage, match_end - 2,
     // literals); zero past the block end
     if (live) {
@@ -368,7 +373,11 @@ __device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int 
 #pragma unroll
     for (int t = 0; t < 8; t++) Z[t] = (uint32_t)__shfl((int)X[t], (int)(jL & 63u), 64);
     const bool okT = can && cT < p && cT >= 4u && Y[1] == X[1];
+#ifdef APE_EXP_NO_L
+    const bool okL = false;
+#else
     const bool okL = can && jL < (uint32_t)lane && cL != cT && Z[1] == X[1];
+#endif
     R.lim = can ? B.mlimit - p : 0u;
 #ifdef APE_EXP_ONE_EAGER
     const bool pickL = okL && !okT;
@@ -377,7 +386,11 @@ __device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int 
 #else
     // measured unconditionally (selects, no branches): every lane reads Y, so the
     // compiler sees the candidate load consumed on every path
+#ifdef APE_EXP_NO_L
+    const uint32_t eT = eager(X, Y), eL = 0u;
+#else
     const uint32_t eT = eager(X, Y), eL = eager(X, Z);
+#endif
     const uint32_t lT = okT ? eT : 0u, lL = okL ? eL : 0u;
     const bool pickL = okL && (!okT || lL > lT || (lL == lT && cL > cT));
 #endif
