@@ -91,6 +91,18 @@ def pmc_traffic(kernel, blocks):
         return None
 
 
+def sq_issue(kernel):
+    """VALU-pipe occupancy of `kernel` from the committed SQ PMC passes (tools/sq_issue.py):
+    the binding resource of this integer byte-shuffling path is instruction issue, not HBM."""
+    p = os.path.join(ROOT, "profiles", "sq_issue.json")
+    try:
+        d = json.load(open(p))[kernel]
+        return {"pipe": "valu", "busy": d["valu_pipe_busy"], "salu_busy": d["salu_busy"],
+                "source": "profiles/sq_issue.json"}
+    except Exception:
+        return None
+
+
 def e2e_bench(args):
     """Host -> GPU -> host rate of the socket path (BASELINE config 5 / north_star e2e).
 
@@ -428,7 +440,8 @@ def main():
             "unit": "GB/s", "frac": round(dom_gbps / HBM_PEAK_GBPS, 4),
             "traffic": pmc_traffic(dom, nb), "kernel": dom,
             "bytes_per_launch": int(alg),
-            "avg_launch_ms": round(enc_ms if enc_ms >= dec_ms else dec_ms, 3)}
+            "avg_launch_ms": round(enc_ms if enc_ms >= dec_ms else dec_ms, 3),
+            "issue": sq_issue(dom)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

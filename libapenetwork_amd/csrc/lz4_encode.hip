@@ -7,34 +7,32 @@
 // last >= 5 bytes are literals -- but it is produced by a chunk-parallel parse,
 // not by the reference's sequential search, so the bytes differ.
 //
-// One 128-thread workgroup (two waves) per block; a batch holds ~1M blocks, so
-// most of the parallelism comes from many blocks in flight.  Per block the LDS
-// holds the reference's own hash table (8192 x u16, 13-bit hash of 5 bytes,
-// :449-462), a 4 KiB ring of recent input and two chunks of match info (~22 KiB,
-// 7 blocks per CU).  The input stays in HBM/L2, read with unaligned 16-byte loads.
+// One 192-thread workgroup (three waves, one role each) per block; a batch holds
+// ~1M blocks, so most of the parallelism comes from many blocks in flight (8 per
+// CU).  Per block the LDS (20.0 KiB) holds the reference's own hash table (8192 x
+// u16, 13-bit hash of 5 bytes, :449-462), a 1 KiB ring of recent input and the
+// hand-over records between the roles.  The input stays in HBM/L2.
 //
-// The block is cut into chunks of 64 positions.  The two waves split the work
-// so that each waits only on its own memory operations (s_waitcnt vmcnt counts a
-// wave's loads and stores together, in order):
-//   PRODUCER (wave 1), software-pipelined one chunk ahead of the consumer:
-//     A(k+2)  load in[p-4, p+28) for every position p of chunk k+2;
-//     B(k+1)  hash in[p, p+5), read candidate T = table[h] (positions walked
-//             earlier, inserted as the reference does: :595-619, :680-706) and
-//             L = the earliest lane of the chunk with the same low hash bits;
-//             issue the load of in[T-4, T+28); copy the chunk into the ring;
-//     C(k)    verify 4 bytes for T and L, measure up to 28 bytes forward and
-//             4 backward, keep the longer (then closer) -> match info in LDS.
-//   CONSUMER (wave 0), one chunk behind:
-//     walk    the greedy chain through chunk k-1 on the scalar unit: jump to the
-//             next lane with a match (ballot mask), catch up backwards into
-//             pending literals (:623-627), extend a match that reached 28 bytes
-//             with the whole wave (1 KiB per step);
-//     table   insert the walked positions and match_end - 2 (:680);
-//     emit    member lanes write their sequences straight to dst (prefix sums
-//             give the offsets); long literal runs and the last literals
-//             (:732-751) are copied by the whole wave with 16-byte moves.
-//   Two workgroup barriers per step keep the table reads of B (before the first)
-//   apart from the consumer's inserts (after it), so the output is deterministic.
+// The block is cut into chunks of 64 positions, one per lane.  The waves run in
+// lock step, two workgroup barriers per step s (each waits only on its own memory
+// operations; s_waitcnt vmcnt counts a wave's loads and stores together, in order):
+//   PRODUCER (wave 1), three chunks in flight:
+//     A(s+3)  load in[p, p+8) for every position p of the chunk;
+//     B(s+2)  hash in[p, p+5), read candidate T = table[h] (positions walked
+//             earlier plus match_end - 2, inserted as the reference does:
+//             :595-619, :680-706) and L = the earliest lane of the chunk with the
+//             same hash bits; copy the chunk into the ring; load in[T-4, T+28);
+//     C1(s+1) verify 4 bytes for T and L, measure both to 28 bytes forward and 4
+//             backward, keep the longer (then closer); load 32 more for a 28;
+//     C2(s)   (second half) finish those to 60 bytes, hash match_end - 2 ->
+//             match info of chunk s in LDS.
+//   WALKER (wave 0), chunk s-1: the greedy chain on the scalar unit (hops over the
+//     match lanes of a ballot mask), catch-up into pending literals (:623-627),
+//     the wave-wide extension of matches >= 60 bytes; second half: table inserts
+//     of the walked positions and match_end - 2 (:680), never overlapping B.
+//   EMITTER (wave 2), chunk s-2: sizes and prefix-sum offsets of the sequences,
+//     then each lane of a 64-byte output window computes its output byte; the
+//     last literals (:732-751) are copied with 16-byte moves.
 #include "lz4_gpu_internal.h"
 #include <type_traits>
 
