@@ -579,7 +579,7 @@ struct Emit {
     uint32_t tot, ex, an, lit, mo;
 };
 
-// First half of step k + 2: sizes and output offsets of chunk k's sequences.
+// Second half of step k + 2: sizes and output offsets of chunk k's sequences.
 __device__ __forceinline__ void emit_prepare(const EncLds &S, const Blk &B, int k, int lane, Emit &E) {
     E.tot = 0;
     const uint64_t members = ((uint64_t)__builtin_amdgcn_readfirstlane(S.wmem[k & 1][1]) << 32) |
@@ -606,16 +606,16 @@ __device__ __forceinline__ void emit_prepare(const EncLds &S, const Blk &B, int 
     }
 }
 
-// Second half of step k + 2: gather.  Lane L of window w produces output byte w + L;
+// First half of step k + 3: gather.  Lane L of window w produces output byte w + L;
 // its sequence is the last member starting at or before it (owner map + prefix max),
 // whose record comes over by ds_bpermute.  One wave's LDS operations complete in
 // order, so the owner-map writes, the read-back and the clearing need no waits.
 __device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int k, int lane, Emit &E) {
     if (!E.members) return;
     const uint32_t P = 64u * (uint32_t)k;
-    // during this half the producer has written chunks up to k + 4, so the ring
-    // holds input [rlo, P + 320)
-    const uint32_t rlo = P + 320u > kRingE ? P + 320u - kRingE : 0u;
+    // runs in the first half of step k + 3, while the producer copies chunk k + 5
+    // into the ring: input [rlo, P + 320) is intact there
+    const uint32_t rlo = P + 384u > kRingE ? P + 384u - kRingE : 0u;
     const bool mem = (E.members >> lane) & 1ull;
     const uint32_t ex = E.ex, tot = E.tot;
     gu8 *out = B.dst + E.o;
@@ -656,9 +656,9 @@ __device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int k, int l
 
 // ---------------- block ----------------
 // Three waves per block, one role each, in lock step (two barriers per step):
-//   step s, first half : producer A(s+3) B(s+2) C1(s+1) | walker walks s-1 | emitter sizes s-2
+//   step s, first half : producer A(s+3) B(s+2) C1(s+1) | walker walks s-1 | emitter writes s-3
 //   step s, second half: producer C2(s) -> info[s%3]     | walker inserts s-1, publishes
-//                                                         | emitter writes s-2
+//                                                         | emitter sizes s-2
 // Table inserts (second half) never overlap the producer's lookups (first half).
 template <bool SMALL>
 __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, int lane,
@@ -748,7 +748,9 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         STATS_FLUSH(g_enc_stats);
         return;
     }
-    // emitter: chunk s-2 during step s
+    // emitter: sizes of chunk s-2 in the second half of step s (the walker published it
+    // in step s-1), its bytes in the first half of step s+1 -- next to the producer's
+    // and the walker's long first halves, so that no half waits on one long role
     Emit E;
     E.o = 0;
     E.overflow = false;
@@ -756,16 +758,22 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
     E.tot = E.ex = E.an = E.lit = E.mo = 0;
     __syncthreads();
     for (int s = 0; s < nsteps; s++) {
-        const bool work = s >= 2 && s <= nch + 1;
-        if (work) emit_prepare(S, B, s - 2, lane, E);
-        STAT(12);
+#ifdef APE_EXP_NOEMIT
+        const bool work = false;   // diagnostic: instruction count without the emitter
+#else
+        const bool work = true;
+#endif
+        if (work && s >= 3 && s <= nch + 2) emit_write(S, B, s - 3, lane, E);
+        STAT(2);
         __syncthreads();
         STAT(14);
-        if (work) emit_write(S, B, s - 2, lane, E);
-        STAT(2);
+        if (work && s >= 2 && s <= nch + 1) emit_prepare(S, B, s - 2, lane, E);
+        STAT(12);
         __syncthreads();
         STAT(15);
     }
+    // nsteps is nch + 2 or nch + 3: the last chunk's bytes may still be pending
+    if (nch >= 1 && nsteps == nch + 2) emit_write(S, B, nch - 1, lane, E);
     // ---- last literals (:732-751), from the walker's final anchor ----
     if (!E.overflow) {
         const uint32_t anchor = S.wend;
