@@ -71,6 +71,31 @@ int APE_LZ4_decompress_safe_partial_batch_dev(const char *const *d_src,
                                               const int *d_maxDecompressedSize,
                                               int *d_result, int nblocks, void *stream);
 
+/* ---- chained streams (socket path with the reference wire format) ----
+ * The reference socket compresses each chunk with compress_fast_continue against the
+ * previous <= 64 KiB of its stream and the receiver decodes it with
+ * decompress_safe_continue against its saved dictionary (ref src/ape_lz4.c:1160-1220,
+ * :1555-1584; src/ape_socket.c:832-857, :1386-1421).  Batched across connections:
+ *
+ * compress_withPrefix : d_prefixSize[i] bytes immediately before d_src[i] are the
+ *   stream's history; matches may reach into it (the last min(prefix, 65536 - size)
+ *   bytes, rounded down to a multiple of 64, are used).  d_result[i] as
+ *   APE_LZ4_compress_batch_dev.  The block decodes with decompress_safe_continue /
+ *   decompress_safe_usingDict given that history (bytes differ from the reference's,
+ *   as for every GPU-compressed block).
+ * decompress_safe_usingDict : == N x APE_LZ4_decompress_safe_usingDict(src, dst,
+ *   csize, cap, dict, dictSize) (ref src/ape_lz4.c:1625-1655), bit-exact, any
+ *   placement of the dictionary (adjacent to dst or not). */
+int APE_LZ4_compress_withPrefix_batch_dev(const char *const *d_src, const int *d_srcSize,
+                                          const int *d_prefixSize, char *const *d_dst,
+                                          const int *d_dstCap, int *d_result, int nblocks,
+                                          void *stream);
+int APE_LZ4_decompress_safe_usingDict_batch_dev(const char *const *d_src,
+                                                const int *d_compressedSize, char *const *d_dst,
+                                                const int *d_maxDecompressedSize,
+                                                const char *const *d_dict, const int *d_dictSize,
+                                                int *d_result, int nblocks, void *stream);
+
 /* ---- batched, device-resident, strided form (block i at base + i*stride) ----
  * The layout the benchmark uses: uncompressed slots of `src_stride` bytes,
  * compressed slots of `dst_stride` bytes; a NULL cap array means

@@ -17,6 +17,7 @@ __all__ = [
     "decompress_safe", "decompress_safe_partial", "compress_batch", "decompress_batch",
     "decompress_partial_batch", "synth_blocks", "gpu_init", "gpu_last_error", "GpuError",
     "MAX_BLOCK", "ERANGE", "frame_offsets", "frame_pack", "decompress_frames",
+    "compress_prefix_batch", "decompress_dict_batch",
 ]
 
 _HERE = _os.path.dirname(_os.path.abspath(__file__))
@@ -62,6 +63,8 @@ def lib():
             "APE_LZ4_frame_offsets_dev": (i, [p, p, p, i, p]),
             "APE_LZ4_frame_pack_strided_dev": (i, [p, sz, p, p, p, i, p]),
             "APE_LZ4_decompress_safe_frames_dev": (i, [p, p, p, sz, p, p, i, p]),
+            "APE_LZ4_compress_withPrefix_batch_dev": (i, [p, p, p, p, p, p, i, p]),
+            "APE_LZ4_decompress_safe_usingDict_batch_dev": (i, [p, p, p, p, p, p, p, i, p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -172,6 +175,26 @@ def decompress_ptr_batch(src_ptrs, comp_sizes, dst_ptrs, caps, results, stream=N
     _check(lib().APE_LZ4_decompress_safe_batch_dev(
         _ptr(src_ptrs), _ptr(comp_sizes), _ptr(dst_ptrs), _ptr(caps), _ptr(results), n,
         _stream(stream)), "APE_LZ4_decompress_safe_batch_dev")
+
+
+def compress_prefix_batch(src_ptrs, src_sizes, prefix_sizes, dst_ptrs, caps, results,
+                          stream=None):
+    """N chained-stream chunks (compress_fast_continue on a stream whose history is the
+    prefix_sizes[i] bytes just before src_ptrs[i]); pointer-array form (int64 tensors)."""
+    n = src_sizes.shape[0]
+    _check(lib().APE_LZ4_compress_withPrefix_batch_dev(
+        _ptr(src_ptrs), _ptr(src_sizes), _ptr(prefix_sizes), _ptr(dst_ptrs), _ptr(caps),
+        _ptr(results), n, _stream(stream)), "APE_LZ4_compress_withPrefix_batch_dev")
+
+
+def decompress_dict_batch(src_ptrs, comp_sizes, dst_ptrs, caps, dict_ptrs, dict_sizes, results,
+                          stream=None):
+    """N x APE_LZ4_decompress_safe_usingDict, pointer-array form (int64 tensors)."""
+    n = comp_sizes.shape[0]
+    _check(lib().APE_LZ4_decompress_safe_usingDict_batch_dev(
+        _ptr(src_ptrs), _ptr(comp_sizes), _ptr(dst_ptrs), _ptr(caps), _ptr(dict_ptrs),
+        _ptr(dict_sizes), _ptr(results), n, _stream(stream)),
+        "APE_LZ4_decompress_safe_usingDict_batch_dev")
 
 
 def synth_blocks(dst, block_size, first_block, kind, stream=None):

@@ -120,6 +120,8 @@ namespace {
 struct Dec {
     gcu8 *src;
     gu8 *dst;
+    gcu8 *dend;      // end of the external dictionary (DICT): history byte -k at dend - k
+    uint32_t dsz;    // dictionary bytes the offset check admits: min(dictSize, 65536), 0 = none
     int csize, cap;
     int64_t oexit;
     int s0;          // staged window start
@@ -162,7 +164,8 @@ __device__ int parse_scalar(WaveLds &L, const Dec &D, int &ip, uint32_t &op, int
     const uint32_t off = sbyte(L, D.src, D.csize, D.s0, ip) |
                          (sbyte(L, D.src, D.csize, D.s0, ip + 1) << 8);  // :1373-1376
     ip += 2;
-    if (cpy - (int64_t)off < 0) { res = -ip - 1; return ST_ERR; }
+    // :1375-1376 (lowLimit = lowPrefix - dictSize; no check once dictSize >= 64 KiB)
+    if (cpy + (int64_t)D.dsz - (int64_t)off < 0) { res = -ip - 1; return ST_ERR; }
     int64_t ml = tok & 15;  // :1379-1391
     if (ml == 15) {
         uint32_t s;
@@ -184,7 +187,7 @@ __device__ int parse_scalar(WaveLds &L, const Dec &D, int &ip, uint32_t &op, int
 // One speculative window at P (P - s0 + kWinNeed <= kStage): appends the
 // chain's descriptors.  Returns ST_MORE with P advanced (to the next token, or
 // to a complex token when `cplx`), or ST_DONE / ST_ERR with `res`.
-template <bool PARTIAL>
+template <bool PARTIAL, bool DICT>
 __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int &nd, int &res,
                             bool &cplx) {
     const int lane = D.lane;
@@ -234,7 +237,7 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const bool fin = fin_in || (PARTIAL ? ((int64_t)cpy > D.oexit) : (cpy + (uint32_t)kMFLimit > ucap));
     const bool badfin = PARTIAL ? (cpy > ucap || iend > (uint32_t)D.csize)
                                 : (iend != (uint32_t)D.csize || cpy > ucap);
-    const bool e_off = cpy < off;                                       // :1375-1376
+    const bool e_off = (DICT ? cpy + D.dsz : cpy) < off;               // :1375-1376
     const bool e_cap = cpy + ml + (uint32_t)(kMinMatch + kLastLiterals) > ucap;   // :1444
     const bool stop = fin || e_off || mlerr || e_cap;
     const bool bad = fin ? badfin : stop;
@@ -279,6 +282,7 @@ __device__ __forceinline__ uint32_t reduce3(uint32_t x, uint32_t off) {
 // Produce output [lo, hi) of the step at `base` from the batch's descriptors.
 // Branch-light: every byte gets an LDS address and (rarely) an HBM pointer; loads
 // are guarded by wave-uniform tests only, so the wave does not juggle exec masks.
+template <bool DICT>
 __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t base, uint32_t lo,
                                           uint32_t hi, uint32_t gdone, int nd, uint32_t d_out) {
     const int lane = D.lane;
@@ -331,14 +335,17 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
         const uint32_t ps = lit ? lpos : mpos;
         const bool live = q >= lo && q < hi && (lit || off != 0u);  // offset 0 -> 0 (App. B)
         const bool inst = ps - s0 < (uint32_t)kStage;
-        const bool ring = !lit && ps >= gdone && ps < lo;
-        const bool pend = live && !lit && ps >= lo;
+        // DICT: a match source before the block start ("negative" ps) is in the dictionary
+        const bool hist = DICT && ps >= 0x80000000u;
+        const bool ring = !lit && !hist && ps >= gdone && ps < lo;
+        const bool pend = live && !lit && !hist && ps >= lo;
         const uint32_t a_st = ps - s0 + (uint32_t)offsetof(WaveLds, stage), a_rg = ps & (kRing - 1);
         const uint32_t a_lit = inst ? a_st : 0xFFFFFFFFu, a_mat = ring ? a_rg : 0xFFFFFFFFu;
         const uint32_t a_live = lit ? a_lit : a_mat;
         pos[j] = ps;
         lad[j] = live ? a_live : 0xFFFFFFFFu;
-        const uint32_t g_lit = inst ? 0u : 1u, g_mat = ps < gdone ? 2u : 0u;
+        const uint32_t g_old = ps < gdone ? 2u : 0u;
+        const uint32_t g_lit = inst ? 0u : 1u, g_mat = hist ? 3u : g_old;
         const uint32_t g_live = lit ? g_lit : g_mat;
         gk[j] = (live && !pend) ? g_live : 0u;
         anyg |= gk[j] != 0u;
@@ -376,7 +383,8 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
                     uint32_t k = x - le;
                     if (k >= d.w) k %= d.w;
                     na = le - d.w + k;
-                    if (na < gdone) ng = 2;
+                    if (DICT && na >= 0x80000000u) ng = 3;
+                    else if (na < gdone) ng = 2;
                     else if (na < lo) nl = na & (kRing - 1);
                     else still = true;
                 }
@@ -403,6 +411,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
             // this CU's L1; the literal in src does not care); idle lanes read src[0]
             gcu8 *bp = gk[j] == 2u ? (gcu8 *)D.dst : D.src;
             const uint32_t o = gk[j] != 0u ? pos[j] : 0u;
+            if (DICT && gk[j] == 3u) bp = D.dend - 0x100000000ll;   // dend + (int32)o
             const uint32_t g = __builtin_nontemporal_load(bp + o);
             v[j] = gk[j] != 0u ? g : v[j];
         }
@@ -433,7 +442,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
 
 }  // namespace
 
-template <bool PARTIAL>
+template <bool PARTIAL, bool DICT>
 __global__ void __launch_bounds__(64)
 lz4_decode_kernel(BlockArgs a) {
     __shared__ WaveLds L;
@@ -455,6 +464,13 @@ lz4_decode_kernel(BlockArgs a) {
     D.oexit = PARTIAL ? a.target[b] : 0;
     if (PARTIAL && D.oexit > (int64_t)D.cap - kMFLimit) D.oexit = (int64_t)D.cap - kMFLimit;
     D.lane = lane;
+    D.dend = nullptr;
+    D.dsz = 0;
+    if (DICT) {   // usingDict (:1625-1647): any placement, adjacent or not, reads the same
+        const int ds = a.dict_size[b] > 0 ? a.dict_size[b] : 0;
+        D.dend = (gcu8 *)a.dict[b] + ds;
+        D.dsz = ds < 65536 ? (uint32_t)ds : 65536u;
+    }
 
     // Special cases of :1316-1318 and the empty-input quirk (the reference reads
     // src[0] even when compressedSize <= 0).
@@ -491,7 +507,7 @@ lz4_decode_kernel(BlockArgs a) {
         while (st == ST_MORE && nd <= kFlushAt) {
             if (P - D.s0 + kWinNeed > kStage) { restage = true; break; }
             bool cplx;
-            st = parse_window<PARTIAL>(L, D, P, op, nd, result, cplx);
+            st = parse_window<PARTIAL, DICT>(L, D, P, op, nd, result, cplx);
             if (st == ST_MORE && cplx) {
                 st = parse_scalar<PARTIAL>(L, D, P, op, nd, result);
                 // a complex token may jump far past the staged bytes
@@ -525,7 +541,7 @@ lz4_decode_kernel(BlockArgs a) {
                 gdone = lo;
             }
             wave_sync();
-            copy_step(L, D, base, lo, hi, gdone, nd, d_out);
+            copy_step<DICT>(L, D, base, lo, hi, gdone, nd, d_out);
             STAT_ADD(3, 1);
         }
         cstart = cend;
@@ -555,10 +571,12 @@ lz4_decode_kernel(BlockArgs a) {
 
 hipError_t launch_decode(const BlockArgs &a, bool partial, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
-    if (partial)
-        hipLaunchKernelGGL(lz4_decode_kernel<true>, dim3(a.nblocks), dim3(64), 0, s, a);
+    if (a.dict)   // usingDict decodes are full decodes (ref :1625-1647)
+        hipLaunchKernelGGL((lz4_decode_kernel<false, true>), dim3(a.nblocks), dim3(64), 0, s, a);
+    else if (partial)
+        hipLaunchKernelGGL((lz4_decode_kernel<true, false>), dim3(a.nblocks), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL(lz4_decode_kernel<false>, dim3(a.nblocks), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((lz4_decode_kernel<false, false>), dim3(a.nblocks), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -275,6 +275,9 @@ struct Blk {
     int n;
     uint32_t un, cap, mstart, mlimit;
     int nch;                         // chunks of 64 positions
+    int k0;                          // first chunk to encode: positions [0, 64 k0) are the
+                                     // history prefix (withPrefix encode), only hashed
+    uint32_t nr;                     // bytes to encode (n - 64 k0)
 };
 
 // ---------------- producer ----------------
@@ -654,6 +657,27 @@ __device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int k, int l
     E.o += tot;
 }
 
+// ---------------- history prefix (withPrefix encode) ----------------
+// Positions [0, 64 k0) precede the block in memory (the previous <= 64 KiB of the
+// stream, as compress_fast_continue sees it, ref src/ape_lz4.c:1160-1220).  The
+// producer wave hashes every one of them into the table, oldest first (one wave:
+// its LDS writes land in order, so the newest position wins deterministically), and
+// copies the last 64 into the ring for the first chunk's backward context.
+__device__ __forceinline__ void prefix_history(EncLds &S, const Blk &B, int lane) {
+    const uint32_t D = 64u * (uint32_t)B.k0;
+    for (uint32_t v0 = 0; v0 < D; v0 += 64u) {
+        const uint32_t v = v0 + (uint32_t)lane;
+        if (v + 8u <= B.un) {   // (the last few of a tiny block stay out of the table)
+            const uint2 x = gload8(B.in + v);
+            S.tab[hash5(x.x, x.y)] = (uint16_t)v;
+        }
+    }
+    const uint32_t p = D - 64u + (uint32_t)lane;
+    const uint8_t by = B.in[p];
+    ((uint8_t *)S.ring)[p & (kRingE - 1)] = by;
+    if (((D - 64u) & (kRingE - 1)) == 0u) ((uint8_t *)S.ring)[kRingE + lane] = by;
+}
+
 // ---------------- block ----------------
 // Three waves per block, one role each, in lock step (two barriers per step):
 //   step s, first half : producer A(s+3) B(s+2) C1(s+1) | walker walks s-1 | emitter writes s-3
@@ -664,8 +688,9 @@ template <bool SMALL>
 __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, int lane,
                                              int *result) {
     STATS_DECL
-    const int nch = B.n >= kMinLength ? B.nch : 0;   // :584, shorter -> last literals only
-    const int nsteps = (nch + 3) & ~1;   // >= nch + 2 steps (emission lags two), even
+    const int k0 = B.k0;
+    const int nch = B.nr >= (uint32_t)kMinLength ? B.nch : k0;   // :584, shorter -> last literals only
+    const int nsteps = k0 + ((nch - k0 + 3) & ~1);   // >= nch + 2 steps (emission lags two)
 
     // Each role runs its own loop (same barrier count: 1 + 2 per step), so the
     // compiler's memory-counter waits in each loop see only that role's operations.
@@ -694,13 +719,14 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             __syncthreads();
             STAT(8);
         };
-        if (nch > 0) {  // prologue: A(0), A(1), B(0), A(2), B(1), C1(0)
-            prod_load<SMALL>(B, 0, lane, P0.X);
-            prod_load<SMALL>(B, 1, lane, P1.X);
-            prod_lookup<SMALL>(S, B, 0, lane, P0.X, P0.cT, P0.jL, P0.h, P0.Y);
-            prod_load<SMALL>(B, 2, lane, P0.X);
-            prod_lookup<SMALL>(S, B, 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
-            prod_measure<SMALL>(S, B, 0, lane, P0.Y, P0.cT, P0.jL, P0.h, P0.q, P0.E);
+        if (k0 > 0) prefix_history(S, B, lane);
+        if (nch > k0) {  // prologue: A(k0), A(k0+1), B(k0), A(k0+2), B(k0+1), C1(k0)
+            prod_load<SMALL>(B, k0, lane, P0.X);
+            prod_load<SMALL>(B, k0 + 1, lane, P1.X);
+            prod_lookup<SMALL>(S, B, k0, lane, P0.X, P0.cT, P0.jL, P0.h, P0.Y);
+            prod_load<SMALL>(B, k0 + 2, lane, P0.X);
+            prod_lookup<SMALL>(S, B, k0 + 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
+            prod_measure<SMALL>(S, B, k0, lane, P0.Y, P0.cT, P0.jL, P0.h, P0.q, P0.E);
         }
         // nothing in flight at the loop entry, so the loop's counter waits depend only
         // on its own issue order (once per block)
@@ -709,9 +735,10 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         // Steps whose three loads all lie inside the block (A(s+3): 64(s+3)+72 <= n,
         // Y(s+2): 64(s+2)+91, E(s+1): 64(s+1)+123) run a loop without the edge paths;
         // the last few steps run the general one.
-        const int nfast = SMALL ? 0 : umin((uint32_t)(B.n >= 264 ? ((B.n - 264) / 64 + 1) & ~1 : 0),
-                                           (uint32_t)nsteps);
-        int s = 0;
+        const int nfast_abs = SMALL ? 0 : (int)umin((uint32_t)(B.n >= 264 ? (B.n - 264) / 64 + 1 : 0),
+                                                    (uint32_t)nsteps);
+        const int nfast = nfast_abs > k0 ? k0 + ((nfast_abs - k0) & ~1) : k0;
+        int s = k0;
         for (; s < nfast; s += 2) {   // no conditional step: see pstep
             pstep(std::true_type{}, s, P0, P1);
             pstep(std::true_type{}, s + 1, P1, P0);
@@ -725,12 +752,12 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
     }
     if (wave == 0) {   // walker: chunk s-1 during step s
         Walk W;
-        W.q = 0;
-        W.anchor = 0;
+        W.q = 64u * (uint32_t)k0;
+        W.anchor = W.q;
         WalkOut O;
         __syncthreads();
-        for (int s = 0; s < nsteps; s++) {
-            const bool work = s >= 1 && s <= nch;
+        for (int s = k0; s < nsteps; s++) {
+            const bool work = s >= k0 + 1 && s <= nch;
             if (work) walk_chunk(S, B, s - 1, lane, W, O);
             STAT(0);
             __syncthreads();
@@ -757,23 +784,23 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
     E.members = 0;
     E.tot = E.ex = E.an = E.lit = E.mo = 0;
     __syncthreads();
-    for (int s = 0; s < nsteps; s++) {
+    for (int s = k0; s < nsteps; s++) {
 #ifdef APE_EXP_NOEMIT
         const bool work = false;   // diagnostic: instruction count without the emitter
 #else
         const bool work = true;
 #endif
-        if (work && s >= 3 && s <= nch + 2) emit_write(S, B, s - 3, lane, E);
+        if (work && s >= k0 + 3 && s <= nch + 2) emit_write(S, B, s - 3, lane, E);
         STAT(2);
         __syncthreads();
         STAT(14);
-        if (work && s >= 2 && s <= nch + 1) emit_prepare(S, B, s - 2, lane, E);
+        if (work && s >= k0 + 2 && s <= nch + 1) emit_prepare(S, B, s - 2, lane, E);
         STAT(12);
         __syncthreads();
         STAT(15);
     }
     // nsteps is nch + 2 or nch + 3: the last chunk's bytes may still be pending
-    if (nch >= 1 && nsteps == nch + 2) emit_write(S, B, nch - 1, lane, E);
+    if (nch > k0 && nsteps == nch + 2) emit_write(S, B, nch - 1, lane, E);
     // ---- last literals (:732-751), from the walker's final anchor ----
     if (!E.overflow) {
         const uint32_t anchor = S.wend;
@@ -810,12 +837,24 @@ lz4_encode_kernel(BlockArgs a) {
     Blk B;
     B.in = (gcu8 *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
     B.dst = (gu8 *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
-    B.n = a.src_size[b];
+    const int nr = a.src_size[b];
     const int icap = a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride;
-    if (B.n < 0 || B.n > kMaxBlock || icap < 0) {
-        if (tid == 0) a.result[b] = (B.n > kMaxBlock) ? kErange : 0;
+    if (nr < 0 || nr > kMaxBlock || icap < 0) {
+        if (tid == 0) a.result[b] = (nr > kMaxBlock) ? kErange : 0;
         return;
     }
+    // withPrefix: the history before the block becomes positions [0, D) of one
+    // 64 KiB window (D a multiple of 64 chunks' worth, so chunk k0 starts the block)
+    int D = 0;
+    if (a.dict_size) {
+        const int pre = a.dict_size[b];
+        D = (pre > 0 ? (pre < kMaxBlock - nr ? pre : kMaxBlock - nr) : 0) & ~63;
+        if (D < 64) D = 0;
+    }
+    B.in -= D;
+    B.n = D + nr;
+    B.nr = (uint32_t)nr;
+    B.k0 = D / 64;
     B.cap = (uint32_t)icap;
     B.un = (uint32_t)B.n;
     B.mstart = B.un >= 12 ? B.un - 12 : 0;   // matches start at <= n-12 (:585)

@@ -124,6 +124,8 @@ struct BlockArgs {
     const int *target;        // partial decode target (nullable)
     const long long *frame_off;  // decoder: blocks read from a framed stream at src_base
                                  // (frame i = [le32 size][block] at src_base + frame_off[i])
+    const char *const *dict;  // decoder: per-block external dictionary (nullable) ...
+    const int *dict_size;     // ... and its size (usingDict, ref src/ape_lz4.c:1625-1647)
     int *result;
     int nblocks;
 };

@@ -261,6 +261,39 @@ int APE_LZ4_decompress_safe_partial_batch_dev(const char *const *d_src,
                          "lz4_decode_kernel<partial>");
 }
 
+int APE_LZ4_decompress_safe_usingDict_batch_dev(const char *const *d_src,
+                                                const int *d_compressedSize, char *const *d_dst,
+                                                const int *d_maxDecompressedSize,
+                                                const char *const *d_dict, const int *d_dictSize,
+                                                int *d_result, int nblocks, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_compressedSize || !d_dst ||
+                                         !d_maxDecompressedSize || !d_dict || !d_dictSize ||
+                                         !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    BlockArgs a = ptr_args(d_src, d_compressedSize, d_dst, d_maxDecompressedSize, nullptr,
+                           d_result, nblocks);
+    a.dict = d_dict;
+    a.dict_size = d_dictSize;
+    return finish_launch(launch_decode(a, false, (hipStream_t)stream),
+                         "lz4_decode_kernel<usingDict>");
+}
+
+int APE_LZ4_compress_withPrefix_batch_dev(const char *const *d_src, const int *d_srcSize,
+                                          const int *d_prefixSize, char *const *d_dst,
+                                          const int *d_dstCap, int *d_result, int nblocks,
+                                          void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_srcSize || !d_prefixSize || !d_dst ||
+                                         !d_dstCap || !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    BlockArgs a = ptr_args(d_src, d_srcSize, d_dst, d_dstCap, nullptr, d_result, nblocks);
+    a.dict_size = d_prefixSize;
+    return finish_launch(launch_encode(a, (hipStream_t)stream), "lz4_encode_kernel<prefix>");
+}
+
 int APE_LZ4_compress_batch_strided_dev(const char *d_src, size_t src_stride, const int *d_srcSize,
                                        char *d_dst, size_t dst_stride, const int *d_dstCap,
                                        int *d_result, int nblocks, void *stream) {
