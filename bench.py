@@ -308,6 +308,118 @@ def rand4k_bench(args):
     print(json.dumps(line), flush=True)
 
 
+def cpu_stream_baseline(n, chunk, target_s):
+    """Reference chained stream on host cores: compress_fast_continue +
+    decompress_safe_continue per chunk, one stream per thread (oracle/cpu_bench.c)."""
+    lib = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
+    lib.cpu_stream_run.restype = C.c_int
+    lib.cpu_stream_run.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                   C.c_int, C.c_int, C.POINTER(C.c_double)]
+    ref = os.path.join(ROOT, "oracle", "_ref", "libape_lz4_ref.so")
+    if os.path.exists(ref):
+        path, prefix, kindname = ref, b"APE_LZ4_", "reference"
+    else:
+        path, prefix, kindname = os.path.join(ROOT, "oracle", "liblz4_oracle.so"), b"orc_", "port"
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    out = (C.c_double * 5)()
+    nb = 1024
+    if lib.cpu_stream_run(path.encode(), prefix, threads, nb, n, chunk, 1, 1, out) != 0:
+        return None
+    per_block = (out[0] + out[1]) / nb
+    nb = int(min(32768, max(1024, target_s / max(per_block, 1e-9) / 2)))
+    reps = max(1, int(target_s / max(per_block * nb, 1e-9)))
+    if lib.cpu_stream_run(path.encode(), prefix, threads, nb, n, chunk, 1, reps, out) != 0 or out[3]:
+        return None
+    tc, td, csz, bytes_ = out[0], out[1], out[2], out[4]
+    return {
+        "value": round(bytes_ * reps / (tc + td) / GIB, 3), "unit": "GiB/s", "cores": threads,
+        "kind": kindname,
+        "sample": "%d threads x one stream each over %d x 64 KiB compressible blocks in %d-byte "
+                  "chunks x %d reps, compress_fast_continue + decompress_safe_continue, %.1f s" % (
+                      threads, nb, chunk, reps, tc + td),
+        "compress_GiBps": round(bytes_ * reps / tc / GIB, 3),
+        "decompress_GiBps": round(bytes_ * reps / td / GIB, 3),
+        "ratio": round(bytes_ / csz, 4),
+    }
+
+
+def stream_bench(args):
+    """Chained-stream socket codec: many connections, 8 KiB chunks,
+    each compressed against its stream's previous bytes (withPrefix) and decoded with
+    them as dictionary (usingDict), device-resident, 1 MI355X.
+
+    Connection b's stream is synthetic block b (64 KiB, App. C); its chunk j has the
+    previous 8 KiB x j bytes of the stream as history (the GPU encoder uses up to
+    65536 - 8192 of them).  A step = TX of all chunks + RX of all chunks."""
+    import torch
+
+    import libapenetwork_amd as amd
+
+    torch.cuda.set_device(0)
+    if amd.gpu_init() != 0:
+        raise SystemExit("GPU codec unavailable: %s" % amd.gpu_last_error())
+    n, ch, nb = 65536, args.stream_chunk, args.stream_blocks
+    per = n // ch
+    nc = nb * per
+    src = torch.empty((nb, n), dtype=torch.uint8, device="cuda")
+    amd.synth_blocks(src, n, 0, 1)
+    cap = amd.compressBound(ch)
+    slot = (cap + 15) // 16 * 16
+    comp = torch.empty((nc, slot), dtype=torch.uint8, device="cuda")
+    out = torch.empty((nb, n), dtype=torch.uint8, device="cuda")
+    j = torch.arange(per, dtype=torch.int64, device="cuda").repeat(nb)
+    b = torch.arange(nb, dtype=torch.int64, device="cuda").repeat_interleave(per)
+    src_ptr = src.data_ptr() + b * n + j * ch
+    dst_ptr = comp.data_ptr() + torch.arange(nc, dtype=torch.int64, device="cuda") * slot
+    out_ptr = out.data_ptr() + b * n + j * ch
+    sizes = torch.full((nc,), ch, dtype=torch.int32, device="cuda")
+    caps = torch.full((nc,), cap, dtype=torch.int32, device="cuda")
+    pre = (j * ch).to(torch.int32)                 # history = the stream so far
+    dict_ptr = src.data_ptr() + b * n               # RX dictionary: the same bytes
+    csz = torch.zeros(nc, dtype=torch.int32, device="cuda")
+    res = torch.zeros(nc, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def tx():
+        amd.compress_prefix_batch(src_ptr, sizes, pre, dst_ptr, caps, csz, stream=stream)
+
+    def rx():
+        amd.decompress_dict_batch(dst_ptr, csz, out_ptr, sizes, dict_ptr, pre, res, stream=stream)
+
+    for _ in range(args.warmup):
+        tx()
+        rx()
+    torch.cuda.synchronize()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    for e in ev:
+        e[0].record(stream)
+        tx()
+        e[1].record(stream)
+        rx()
+        e[2].record(stream)
+    torch.cuda.synchronize()
+    tx_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    rx_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    ok = bool((res == ch).all().item()) and bool(torch.equal(out, src))
+    cbytes = int(csz.to(torch.int64).sum().item())
+    cpu = None if args.no_cpu_baseline else cpu_stream_baseline(n, ch, args.cpu_seconds)
+    line = {
+        "metric": "LZ4 GiB/s chained-stream socket codec (withPrefix TX + usingDict RX), "
+                  "%d-byte chunks" % ch,
+        "value": round(nb * n / ((tx_ms + rx_ms) * 1e-3) / GIB, 2), "unit": "GiB/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(tx_ms + rx_ms, 3), "higher_is_better": True, "dtype": "u8",
+        "data": "synthetic (SURVEY App. C gen_comp, one stream per block)",
+        "config": {"workload": "%d connections x 64 KiB streams = %d chunks of %d B, history "
+                               "up to 64 KiB" % (nb, nc, ch)},
+        "tx_ms": round(tx_ms, 3), "rx_ms": round(rx_ms, 3),
+        "tx_GiBps": round(nb * n / (tx_ms * 1e-3) / GIB, 2),
+        "rx_GiBps": round(nb * n / (rx_ms * 1e-3) / GIB, 2),
+        "ratio": round(nb * n / cbytes, 4), "verified": ok, "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -326,9 +438,15 @@ def main():
     ap.add_argument("--rand4k", action="store_true",
                     help="BASELINE config 2: decompress-only over 4 KiB random blocks")
     ap.add_argument("--rand4k-blocks", type=int, default=1 << 18)
+    ap.add_argument("--stream", action="store_true",
+                    help="chained-stream socket codec (withPrefix TX + usingDict RX)")
+    ap.add_argument("--stream-blocks", type=int, default=1 << 17)
+    ap.add_argument("--stream-chunk", type=int, default=8192)
     args = ap.parse_args()
     if args.e2e:
         return e2e_bench(args)
+    if args.stream:
+        return stream_bench(args)
     if args.rand4k:
         return rand4k_bench(args)
 

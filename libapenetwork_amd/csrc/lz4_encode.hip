@@ -660,16 +660,26 @@ __device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int k, int l
 // ---------------- history prefix (withPrefix encode) ----------------
 // Positions [0, 64 k0) precede the block in memory (the previous <= 64 KiB of the
 // stream, as compress_fast_continue sees it, ref src/ape_lz4.c:1160-1220).  The
-// producer wave hashes every one of them into the table, oldest first (one wave:
-// its LDS writes land in order, so the newest position wins deterministically), and
-// copies the last 64 into the ring for the first chunk's backward context.
+// producer wave hashes every third of them into the table, as loadDict does
+// (:1127-1130; catch-up recovers the bytes a skipped start loses), oldest first (one
+// wave: its LDS writes land in order, so the newest position wins deterministically),
+// and copies the last 64 into the ring for the first chunk's backward context.
 __device__ __forceinline__ void prefix_history(EncLds &S, const Blk &B, int lane) {
     const uint32_t D = 64u * (uint32_t)B.k0;
-    for (uint32_t v0 = 0; v0 < D; v0 += 64u) {
-        const uint32_t v = v0 + (uint32_t)lane;
-        if (v + 8u <= B.un) {   // (the last few of a tiny block stay out of the table)
-            const uint2 x = gload8(B.in + v);
-            S.tab[hash5(x.x, x.y)] = (uint16_t)v;
+    constexpr int kU = 8;   // loads in flight per trip (the loop is latency bound)
+    for (uint32_t v0 = 0; v0 < D; v0 += 192u * kU) {
+        uint2 x[kU];
+        bool ok[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t v = v0 + 192u * u + 3u * (uint32_t)lane;
+            ok[u] = v < D && v + 8u <= B.un;   // (the last few of a tiny block stay out)
+            x[u] = gload8(B.in + (ok[u] ? v : 0u));
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t v = v0 + 192u * u + 3u * (uint32_t)lane;
+            if (ok[u]) S.tab[hash5(x[u].x, x[u].y)] = (uint16_t)v;
         }
     }
     const uint32_t p = D - 64u + (uint32_t)lane;

@@ -121,3 +121,117 @@ int cpu_bench_run(const char *lib, const char *prefix, int nthreads, int nblocks
     dlclose(h);
     return 0;
 }
+
+/*
+ * Chained-stream baseline (the reference socket's codec use):
+ * each thread runs one stream over its contiguous range of blocks, cut into
+ * `chunk`-byte pieces -- TX compress_fast_continue per chunk on one stream state
+ * (history = the previous input, in place, as ape_socket.c:832 sees it), RX
+ * decompress_safe_continue per chunk into one contiguous output (prefix mode,
+ * ape_lz4.c:1555-1584).  Same out[] layout as cpu_bench_run (bytes = payload).
+ */
+typedef void *(*mk_fn)(void);
+typedef int (*free_fn)(void *);
+typedef int (*ccont_fn)(void *, const char *, char *, int, int, int);
+typedef int (*dcont_fn)(void *, const char *, char *, int, int);
+
+typedef struct {
+    mk_fn mk, mkd;
+    free_fn fr, frd;
+    ccont_fn cc;
+    dcont_fn dc;
+    const uint8_t *in;
+    uint8_t *cmp, *out;
+    int *csz;
+    long long c0, c1;   /* chunk range */
+    int chunk, cap, phase, bad;
+} stask_t;
+
+static void *sworker(void *arg)
+{
+    stask_t *t = (stask_t *)arg;
+    if (t->phase == 0) {
+        void *s = t->mk();
+        for (long long c = t->c0; c < t->c1; c++)
+            t->csz[c] = t->cc(s, (const char *)t->in + c * t->chunk, (char *)t->cmp + c * t->cap,
+                              t->chunk, t->cap, 1);
+        t->fr(s);
+    } else {
+        void *d = t->mkd();
+        for (long long c = t->c0; c < t->c1; c++) {
+            int r = t->dc(d, (const char *)t->cmp + c * t->cap, (char *)t->out + c * t->chunk,
+                          t->csz[c], t->chunk);
+            if (r != t->chunk) t->bad++;
+        }
+        t->frd(d);
+    }
+    return NULL;
+}
+
+static double run_sphase(stask_t *tasks, int nthreads, int phase)
+{
+    pthread_t th[256];
+    double t0 = now_s();
+    for (int i = 0; i < nthreads; i++) {
+        tasks[i].phase = phase;
+        pthread_create(&th[i], NULL, sworker, &tasks[i]);
+    }
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    return now_s() - t0;
+}
+
+int cpu_stream_run(const char *lib, const char *prefix, int nthreads, int nblocks, int n,
+                   int chunk, int kind, int reps, double *out)
+{
+    char name[128];
+    void *h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+    if (!h) { fprintf(stderr, "cpu_bench: %s\n", dlerror()); return -1; }
+#define SYM(var, type, nm) snprintf(name, sizeof name, "%s" nm, prefix); type var = (type)dlsym(h, name)
+    SYM(mk, mk_fn, "createStream");
+    SYM(fr, free_fn, "freeStream");
+    SYM(mkd, mk_fn, "createStreamDecode");
+    SYM(frd, free_fn, "freeStreamDecode");
+    SYM(cc, ccont_fn, "compress_fast_continue");
+    SYM(dc, dcont_fn, "decompress_safe_continue");
+#undef SYM
+    if (!mk || !fr || !mkd || !frd || !cc || !dc || nthreads < 1 || nthreads > 256 ||
+        chunk <= 0 || n % chunk)
+        return -2;
+    const int cap = chunk + chunk / 255 + 16;
+    const long long nch = (long long)nblocks * (n / chunk);
+    uint8_t *in = malloc((size_t)nblocks * n);
+    uint8_t *cmp = malloc((size_t)nch * cap);
+    uint8_t *o = malloc((size_t)nblocks * n);
+    int *csz = calloc((size_t)nch, sizeof(int));
+    if (!in || !cmp || !o || !csz) return -3;
+    synth_blocks(in, n, n, 0, nblocks, kind);
+    memset(cmp, 0, (size_t)nch * cap);
+    memset(o, 0, (size_t)nblocks * n);
+    stask_t tasks[256];
+    for (int i = 0; i < nthreads; i++) {
+        /* whole blocks per thread, so every stream starts at a block boundary */
+        const long long b0 = (long long)nblocks * i / nthreads, b1 = (long long)nblocks * (i + 1) / nthreads;
+        tasks[i] = (stask_t){mk, mkd, fr, frd, cc, dc, in, cmp, o, csz,
+                             b0 * (n / chunk), b1 * (n / chunk), chunk, cap, 0, 0};
+    }
+    run_sphase(tasks, nthreads, 0); /* warm-up */
+    run_sphase(tasks, nthreads, 1);
+    double tc = 0, td = 0;
+    for (int r = 0; r < reps; r++) {
+        tc += run_sphase(tasks, nthreads, 0);
+        td += run_sphase(tasks, nthreads, 1);
+    }
+    long long tot = 0;
+    int bad = 0;
+    for (long long c = 0; c < nch; c++) tot += csz[c];
+    for (int i = 0; i < nthreads; i++) bad += tasks[i].bad;
+    if (memcmp(in, o, (size_t)nblocks * n) != 0) bad++;
+    out[0] = tc;
+    out[1] = td;
+    out[2] = (double)tot;
+    out[3] = bad;
+    out[4] = (double)nblocks * n;
+    free(in); free(cmp); free(o); free(csz);
+    dlclose(h);
+    return 0;
+}
