@@ -29,6 +29,7 @@
 //         owner map).  Output goes to the ring and straight to dst.
 // Decoded blocks are not limited to 64 KiB: only the 64 KiB offset window is.
 #include "lz4_gpu_internal.h"
+#include <type_traits>
 
 namespace apelz4 {
 
@@ -313,43 +314,61 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
         if (needmod) rA %= offA;
     }
 
-    // per byte: source position, LDS address (0xFFFFFFFF = none), HBM kind (1 src, 2 dst)
+    // per byte: source position, LDS address (kNone = a zero byte), HBM kind (1 src,
+    // 2 dst, 3 dictionary).  Two wave-uniform specialisations: FULL (the step is
+    // produced whole: no range test) and SO (some lane's offset is 1..3: its period
+    // needs up to three reductions; otherwise one conditional subtraction covers
+    // rA + j < off + 3 and q - le <= 2).
+    constexpr uint32_t kNone = (uint32_t)offsetof(WaveLds, stage) + (uint32_t)kStage;
     uint32_t pos[4], lad[4], gk[4];
     uint32_t pendm = 0;
     bool anyg = false;
+    auto bytes = [&](auto so_t, auto full_t) {
+        constexpr bool SO = decltype(so_t)::value, FU = decltype(full_t)::value;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        // Every arm is computed into a variable first and the ternaries only pick
-        // between plain values: the compiler then emits v_cndmask selects, not the
-        // divergent branches (exec-mask juggling on the scalar unit) that nested
-        // ternaries with arithmetic in their arms become.
-        const uint32_t q = q0 + j;
-        const bool inB = q >= outB;
-        const uint32_t le = inB ? leB : leA, off = inB ? offB : offA, xl = inB ? xlB : xlA;
-        const bool lit = q < le;
-        const uint32_t mbB = q - leB, mbA0 = rA + j, mbA1 = q - leA;
-        const uint32_t mbA = q0 >= leA ? mbA0 : mbA1;
-        const uint32_t mb = inB ? mbB : mbA;
-        const uint32_t mpos = le - off + reduce3(mb, off);
-        const uint32_t lpos = q + xl;
-        const uint32_t ps = lit ? lpos : mpos;
-        const bool live = q >= lo && q < hi && (lit || off != 0u);  // offset 0 -> 0 (App. B)
-        const bool inst = ps - s0 < (uint32_t)kStage;
-        // DICT: a match source before the block start ("negative" ps) is in the dictionary
-        const bool hist = DICT && ps >= 0x80000000u;
-        const bool ring = !lit && !hist && ps >= gdone && ps < lo;
-        const bool pend = live && !lit && !hist && ps >= lo;
-        const uint32_t a_st = ps - s0 + (uint32_t)offsetof(WaveLds, stage), a_rg = ps & (kRing - 1);
-        const uint32_t a_lit = inst ? a_st : 0xFFFFFFFFu, a_mat = ring ? a_rg : 0xFFFFFFFFu;
-        const uint32_t a_live = lit ? a_lit : a_mat;
-        pos[j] = ps;
-        lad[j] = live ? a_live : 0xFFFFFFFFu;
-        const uint32_t g_old = ps < gdone ? 2u : 0u;
-        const uint32_t g_lit = inst ? 0u : 1u, g_mat = hist ? 3u : g_old;
-        const uint32_t g_live = lit ? g_lit : g_mat;
-        gk[j] = (live && !pend) ? g_live : 0u;
-        anyg |= gk[j] != 0u;
-        pendm |= pend ? 1u << j : 0u;
+        for (int j = 0; j < 4; j++) {
+            // Every arm is computed into a variable first and the ternaries only pick
+            // between plain values: the compiler then emits v_cndmask selects, not the
+            // divergent branches (exec-mask juggling on the scalar unit) that nested
+            // ternaries with arithmetic in their arms become.
+            const uint32_t q = q0 + j;
+            const bool inB = q >= outB;
+            const uint32_t le = inB ? leB : leA, off = inB ? offB : offA, xl = inB ? xlB : xlA;
+            const bool lit = q < le;
+            const uint32_t mbB = q - leB, mbA0 = rA + j, mbA1 = q - leA;
+            const uint32_t mbA = q0 >= leA ? mbA0 : mbA1;
+            const uint32_t mb = inB ? mbB : mbA;
+            const uint32_t red = SO ? reduce3(mb, off) : umin(mb, mb - off);
+            const uint32_t mpos = le - off + red;
+            const uint32_t lpos = q + xl;
+            const uint32_t ps = lit ? lpos : mpos;
+            const bool live = (FU || (q >= lo && q < hi)) && (lit || off != 0u);  // offset 0 -> 0
+            const bool inst = ps - s0 < (uint32_t)kStage;
+            // DICT: a match source before the block start ("negative" ps) is in the dictionary
+            const bool hist = DICT && ps >= 0x80000000u;
+            const bool ring = !lit && !hist && ps >= gdone && ps < lo;
+            const bool pend = live && !lit && !hist && ps >= lo;
+            const uint32_t a_st = ps - s0 + (uint32_t)offsetof(WaveLds, stage), a_rg = ps & (kRing - 1);
+            const uint32_t a_lit = inst ? a_st : kNone, a_mat = ring ? a_rg : kNone;
+            const uint32_t a_live = lit ? a_lit : a_mat;
+            pos[j] = ps;
+            lad[j] = live ? a_live : kNone;
+            const uint32_t g_old = ps < gdone ? 2u : 0u;
+            const uint32_t g_lit = inst ? 0u : 1u, g_mat = hist ? 3u : g_old;
+            const uint32_t g_live = lit ? g_lit : g_mat;
+            gk[j] = (live && !pend) ? g_live : 0u;
+            anyg |= gk[j] != 0u;
+            pendm |= pend ? 1u << j : 0u;
+        }
+    };
+    const bool so = offA - 1u < 3u || offB - 1u < 3u;
+    const bool full = lo == base && hi == base + kStep;
+    if (__any(so)) {
+        if (full) bytes(std::true_type{}, std::true_type{});
+        else bytes(std::true_type{}, std::false_type{});
+    } else {
+        if (full) bytes(std::false_type{}, std::true_type{});
+        else bytes(std::false_type{}, std::false_type{});
     }
     // in-step sources: follow them through the owner map (short chains, rare)
     if (__any(pendm != 0)) {
@@ -371,7 +390,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
                     if (j == j0) x = pos[j];
                 const uint4 d = L.desc[((const uint8_t *)L.own)[x - base] - 1u];
                 const uint32_t le = d.y + d.z;
-                uint32_t na, nl = 0xFFFFFFFFu, ng = 0;
+                uint32_t na, nl = kNone, ng = 0;
                 bool still = false;
                 if (x < le) {
                     na = d.x + (x - d.y);
@@ -396,14 +415,11 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
             }
         }
     }
-    // fetch: LDS for every byte (invalid addresses read 0), HBM only if a lane needs it
+    // fetch: LDS for every byte, HBM only if a lane needs it
     const uint8_t *lds = (const uint8_t *)&L;
     uint32_t v[4];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t lv = lds[lad[j] & 0xFFFFu];   // unconditional (out of range reads 0)
-        v[j] = lad[j] != 0xFFFFFFFFu ? lv : 0u;
-    }
+    for (int j = 0; j < 4; j++) v[j] = lds[lad[j]];   // kNone reads 0
     if (__any(anyg)) {
 #pragma unroll
         for (int j = 0; j < 4; j++) {
