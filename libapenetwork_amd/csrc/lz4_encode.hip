@@ -574,68 +574,95 @@ __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int
 }
 
 // ---------------- emitter ----------------
-struct Emit {
-    uint32_t o;          // output cursor
-    bool overflow;
-    // chunk being emitted (set in the first half, used in the second)
+// Chunks are emitted in pairs (one 64-byte output window holds ~40 bytes of two
+// chunks' sequences instead of ~20 of one): sizes of each chunk in the second half
+// of step k + 2, both chunks' bytes in the first half of step kA + 4 (kA = the pair's
+// first chunk).
+struct EmitC {          // one chunk's sequences, per member lane
     uint64_t members;
     uint32_t tot, ex, an, lit, mo;
 };
+struct Emit {
+    uint32_t o;          // output cursor
+    bool overflow;
+    bool pend;           // A (and B) prepared, not yet written
+    int kA;              // first chunk of the pending pair
+    EmitC A, Bc;
+};
 
-// Second half of step k + 2: sizes and output offsets of chunk k's sequences.
-__device__ __forceinline__ void emit_prepare(const EncLds &S, const Blk &B, int k, int lane, Emit &E) {
-    E.tot = 0;
+// Sizes and output offsets of chunk k's sequences into C; `before` = output bytes of
+// the pair's earlier chunk.
+__device__ __forceinline__ void emit_prepare(const EncLds &S, const Blk &B, int k, int lane, Emit &E,
+                                             EmitC &C, uint32_t before) {
+    C.tot = 0;
     const uint64_t members = ((uint64_t)__builtin_amdgcn_readfirstlane(S.wmem[k & 1][1]) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane(S.wmem[k & 1][0]);
-    E.members = E.overflow ? 0ull : members;
-    if (!E.members) return;
+    C.members = E.overflow ? 0ull : members;
+    if (!C.members) return;
     const uint2 wr = S.wres[k & 1][lane];
     const uint32_t off = S.info[k % 3][lane].y & 0xFFFFu;
-    const bool mem = (E.members >> lane) & 1ull;
+    const bool mem = (C.members >> lane) & 1ull;
     const uint32_t m_len = wr.x & 0xFFFFFu, m_back = wr.x >> 20;
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const uint32_t ms = p - m_back;            // match start after catch-up
-    E.an = wr.y;
-    E.lit = mem ? ms - E.an : 0u;
+    C.an = wr.y;
+    C.lit = mem ? ms - C.an : 0u;
     const uint32_t ml = m_len - kMinMatch;
-    const uint32_t size = mem ? 1u + ext_bytes(E.lit) + E.lit + 2u + ext_bytes(ml) : 0u;
-    E.ex = wave_excl_scan(size);
-    E.tot = lane_val(E.ex + size, 63);
-    E.mo = ml | (off << 16);
-    if ((uint64_t)E.o + E.tot > B.cap) {
+    const uint32_t size = mem ? 1u + ext_bytes(C.lit) + C.lit + 2u + ext_bytes(ml) : 0u;
+    C.ex = wave_excl_scan(size);
+    C.tot = lane_val(C.ex + size, 63);
+    C.mo = ml | (off << 16);
+    if ((uint64_t)E.o + before + C.tot > B.cap) {
         E.overflow = true;
-        E.members = 0;
-        E.tot = 0;
+        C.members = 0;
+        C.tot = 0;
     }
 }
 
-// First half of step k + 3: gather.  Lane L of window w produces output byte w + L;
-// its sequence is the last member starting at or before it (owner map + prefix max),
-// whose record comes over by ds_bpermute.  One wave's LDS operations complete in
-// order, so the owner-map writes, the read-back and the clearing need no waits.
-__device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int k, int lane, Emit &E) {
-    if (!E.members) return;
-    const uint32_t P = 64u * (uint32_t)k;
-    // runs in the first half of step k + 3, while the producer copies chunk k + 5
-    // into the ring: input [rlo, P + 320) is intact there
-    const uint32_t rlo = P + 384u > kRingE ? P + 384u - kRingE : 0u;
-    const bool mem = (E.members >> lane) & 1ull;
-    const uint32_t ex = E.ex, tot = E.tot;
+// Gather the pair (kA, kA + 1).  Lane L of window w produces output byte w + L; its
+// sequence is the last member starting at or before it (owner map + prefix max over
+// owners 1..64 = chunk A's lanes, 65..128 = chunk B's, B's all after A's), whose
+// record comes over by ds_bpermute.  One wave's LDS operations complete in order, so
+// the owner-map writes, the read-back and the clearing need no waits.
+__device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int kA, int lane, Emit &E) {
+    const uint32_t totA = E.A.tot, tot = totA + E.Bc.tot;
+    if (tot == 0) return;
+    const uint32_t P = 64u * (uint32_t)kA;
+    // runs in the first half of step kA + 4, while the producer copies chunk kA + 6
+    // into the ring (or after the last step): input [rlo, P + 384) is intact there
+    const uint32_t rlo = P + 448u > kRingE ? P + 448u - kRingE : 0u;
+    const bool memA = (E.A.members >> lane) & 1ull, memB = (E.Bc.members >> lane) & 1ull;
+    const uint32_t exA = E.A.ex, exB = totA + E.Bc.ex;
     gu8 *out = B.dst + E.o;
     for (uint32_t w = 0; w < tot; w += 64u) {
-        const bool mark = mem && ex > w && ex < w + 64u;
-        if (mark) ((uint8_t *)S.omap)[ex - w] = (uint8_t)(lane + 1);
+        const bool markA = memA && exA > w && exA < w + 64u;
+        const bool markB = memB && exB > w && exB < w + 64u;
+        if (markA) ((uint8_t *)S.omap)[exA - w] = (uint8_t)(lane + 1);
+        if (markB) ((uint8_t *)S.omap)[exB - w] = (uint8_t)(lane + 65);
         __builtin_amdgcn_sched_barrier(0);
         const uint32_t mk = ((const uint8_t *)S.omap)[lane];
         __builtin_amdgcn_sched_barrier(0);
-        if (mark) ((uint8_t *)S.omap)[ex - w] = 0;
-        const uint64_t cov = __ballot(mem && ex <= w);   // member 0 starts at 0
-        const uint32_t carry = 64u - (uint32_t)__clzll((long long)cov);
-        const int own = (int)(umax(wave_incl_max(mk), carry) - 1u);
-        const uint32_t r_ex = (uint32_t)__builtin_amdgcn_ds_bpermute(own << 2, (int)ex);
-        const uint32_t r_an = (uint32_t)__builtin_amdgcn_ds_bpermute(own << 2, (int)E.an);
-        const uint32_t rl = (uint32_t)__builtin_amdgcn_ds_bpermute(own << 2, (int)E.lit);
-        const uint32_t r_mo = (uint32_t)__builtin_amdgcn_ds_bpermute(own << 2, (int)E.mo);
+        if (markA) ((uint8_t *)S.omap)[exA - w] = 0;
+        if (markB) ((uint8_t *)S.omap)[exB - w] = 0;
+        const uint64_t covA = __ballot(memA && exA <= w);   // member 0 of A starts at 0
+        const uint64_t covB = __ballot(memB && exB <= w);
+        const uint32_t carry = covB ? 128u - (uint32_t)__clzll((long long)covB)
+                                    : 64u - (uint32_t)__clzll((long long)covA);
+        const uint32_t own = umax(wave_incl_max(mk), carry) - 1u;
+        const int sl = (int)((own & 63u) << 2);
+        const bool fb = own >= 64u;
+        // all eight permutes by every lane (a permute reads its source lane's register,
+        // so it must not run under a lane-dependent condition), then a select
+        const uint32_t a_ex = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)exA);
+        const uint32_t b_ex = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)exB);
+        const uint32_t a_an = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.an);
+        const uint32_t b_an = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.an);
+        const uint32_t a_li = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.lit);
+        const uint32_t b_li = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.lit);
+        const uint32_t a_mo = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.mo);
+        const uint32_t b_mo = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.mo);
+        const uint32_t r_ex = fb ? b_ex : a_ex, r_an = fb ? b_an : a_an;
+        const uint32_t rl = fb ? b_li : a_li, r_mo = fb ? b_mo : a_mo;
         const uint32_t b = w + (uint32_t)lane;
         // every candidate value computed, then selected (no divergent branches)
         const uint32_t rr = b - r_ex;                    // offset inside the sequence
@@ -690,7 +717,8 @@ __device__ __forceinline__ void prefix_history(EncLds &S, const Blk &B, int lane
 
 // ---------------- block ----------------
 // Three waves per block, one role each, in lock step (two barriers per step):
-//   step s, first half : producer A(s+3) B(s+2) C1(s+1) | walker walks s-1 | emitter writes s-3
+//   step s, first half : producer A(s+3) B(s+2) C1(s+1) | walker walks s-1 | emitter writes
+//                                                         |   the pair (s-4, s-3) (every 2nd step)
 //   step s, second half: producer C2(s) -> info[s%3]     | walker inserts s-1, publishes
 //                                                         | emitter sizes s-2
 // Table inserts (second half) never overlap the producer's lookups (first half).
@@ -786,13 +814,16 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         return;
     }
     // emitter: sizes of chunk s-2 in the second half of step s (the walker published it
-    // in step s-1), its bytes in the first half of step s+1 -- next to the producer's
-    // and the walker's long first halves, so that no half waits on one long role
+    // in step s-1); the bytes of a pair (kA, kA+1) in the first half of step kA+4 --
+    // next to the producer's and the walker's long first halves
     Emit E;
     E.o = 0;
     E.overflow = false;
-    E.members = 0;
-    E.tot = E.ex = E.an = E.lit = E.mo = 0;
+    E.pend = false;
+    E.kA = k0;
+    E.A.members = E.Bc.members = 0;
+    E.A.tot = E.A.ex = E.A.an = E.A.lit = E.A.mo = 0;
+    E.Bc.tot = E.Bc.ex = E.Bc.an = E.Bc.lit = E.Bc.mo = 0;
     __syncthreads();
     for (int s = k0; s < nsteps; s++) {
 #ifdef APE_EXP_NOEMIT
@@ -800,17 +831,31 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
 #else
         const bool work = true;
 #endif
-        if (work && s >= k0 + 3 && s <= nch + 2) emit_write(S, B, s - 3, lane, E);
+        const int r = s - k0;
+        if (work && E.pend && E.kA == s - 4) {   // the pair prepared in steps s-2, s-1
+            emit_write(S, B, s - 4, lane, E);
+            E.pend = false;
+        }
         STAT(2);
         __syncthreads();
         STAT(14);
-        if (work && s >= k0 + 2 && s <= nch + 1) emit_prepare(S, B, s - 2, lane, E);
+        if (work && r >= 2 && s - 2 < nch) {
+            if (((r - 2) & 1) == 0) {            // first chunk of a pair
+                E.Bc.members = 0;
+                E.Bc.tot = 0;
+                emit_prepare(S, B, s - 2, lane, E, E.A, 0u);
+                E.kA = s - 2;
+                E.pend = true;
+            } else {
+                emit_prepare(S, B, s - 2, lane, E, E.Bc, E.A.tot);
+            }
+        }
         STAT(12);
         __syncthreads();
         STAT(15);
     }
-    // nsteps is nch + 2 or nch + 3: the last chunk's bytes may still be pending
-    if (nch > k0 && nsteps == nch + 2) emit_write(S, B, nch - 1, lane, E);
+    // the last pair may still be pending (its write step lies past the loop)
+    if (E.pend) emit_write(S, B, E.kA, lane, E);
     // ---- last literals (:732-751), from the walker's final anchor ----
     if (!E.overflow) {
         const uint32_t anchor = S.wend;
