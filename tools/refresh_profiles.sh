@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round profile refresh on the GPU box (results under gpurun_out/; copy into profiles/
+# with tools/collect_profiles.sh here): the headline bench line + rocprofv3 kernel stats
+# of the same command, SQ issue passes, PMC FETCH_SIZE / WRITE_SIZE passes, and the
+# secondary bench lines (--stream, --rand4k, --e2e).
+set -o pipefail
+TAG=${1:-r1}
+cd /tmp && export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+bash tools/gpu_bench.sh $TAG || exit 1
+bash tools/sq_passes.sh 16384 > gpurun_out/sq_$TAG.txt 2>&1 || { tail -5 gpurun_out/sq_$TAG.txt; exit 1; }
+NB=65536
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv -- python3 bench.py --blocks $NB --steps 1 --warmup 0 --no-cpu-baseline --verify-sample 0 > gpurun_out/pmc_$c.log 2>&1 || { echo "pass $c failed"; tail -5 gpurun_out/pmc_$c.log; exit 1; }
+done
+timeout -k 10 400 python3 -u bench.py --stream > gpurun_out/stream_$TAG.json 2> gpurun_out/stream_$TAG.err || exit 1
+timeout -k 10 300 python3 -u bench.py --rand4k > gpurun_out/rand4k_$TAG.json 2> gpurun_out/rand4k_$TAG.err || exit 1
+timeout -k 10 300 python3 -u bench.py --e2e > gpurun_out/e2e_$TAG.json 2> gpurun_out/e2e_$TAG.err || exit 1
+cat gpurun_out/stream_$TAG.json gpurun_out/rand4k_$TAG.json gpurun_out/e2e_$TAG.json
