@@ -57,7 +57,8 @@ namespace {
 #endif
 constexpr int kHLog = APE_LZ4_HLOG;
 constexpr int kHSize = 1 << kHLog;
-constexpr uint32_t kEagerLen = 28;   // match bytes measured by the producer
+constexpr uint32_t kEagerLen = 28;   // match bytes measured by the producer (T candidate)
+constexpr uint32_t kEagerL = 12;     // ... for the in-chunk candidate L
 #ifndef APE_LZ4_ERING
 #define APE_LZ4_ERING 1024
 #endif
@@ -68,7 +69,6 @@ constexpr uint32_t kRingE = APE_LZ4_ERING;  // recent input bytes (own, stage 2,
 constexpr uint32_t kScr = 1u << APE_LZ4_SCRBITS;  // in-chunk candidate scratch entries
 constexpr int kSmall = 128;          // smaller blocks take the byte-load path
 
-constexpr uint32_t kEager2 = kEagerLen + 32;  // after the producer's second stage
 
 // info.x: len (8) | back << 8 (3) | trunc << 11 | has << 12 | hashable << 13 |
 //         e2 << 14 | hash(match_end - 2) << 16;   info.y: offset | h << 16
@@ -282,7 +282,7 @@ struct Blk {
 
 // ---------------- producer ----------------
 struct Part {                        // C1 result of one chunk, finished by C2
-    uint32_t len, c, bk, lim, h;
+    uint32_t len, c, bk, lim, h, base;   // base: bytes C1 measured (kEagerLen / kEagerL)
     bool has, hashable, trunc1;
 };
 
@@ -370,9 +370,12 @@ __device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int 
     R.hashable = live && p + 5u <= B.un;
     const bool can = live && p >= 1u && p <= B.mstart && B.n >= kMinLength;
     const uint32_t cL = 64u * (uint32_t)k + jL;
+    // L candidate bytes in[cL-4, cL+12) from lane jL's own bytes
     uint32_t Z[8];
 #pragma unroll
-    for (int t = 0; t < 8; t++) Z[t] = (uint32_t)__shfl((int)X[t], (int)(jL & 63u), 64);
+    for (int t = 0; t < 4; t++) Z[t] = (uint32_t)__shfl((int)X[t], (int)(jL & 63u), 64);
+#pragma unroll
+    for (int t = 4; t < 8; t++) Z[t] = 0u;
     const bool okT = can && cT < p && cT >= 4u && Y[1] == X[1];
 #ifdef APE_EXP_NO_L
     const bool okL = false;
@@ -380,29 +383,24 @@ __device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int 
     const bool okL = can && jL < (uint32_t)lane && cL != cT && Z[1] == X[1];
 #endif
     R.lim = can ? B.mlimit - p : 0u;
-#ifdef APE_EXP_ONE_EAGER
-    const bool pickL = okL && !okT;
-    const uint32_t lT = pickL ? 0u : (okT ? eager(X, Y) : 0u);
-    const uint32_t lL = pickL ? eager(X, Z) : 0u;
-#else
     // measured unconditionally (selects, no branches): every lane reads Y, so the
-    // compiler sees the candidate load consumed on every path
-#ifdef APE_EXP_NO_L
-    const uint32_t eT = eager(X, Y), eL = 0u;
-#else
-    const uint32_t eT = eager(X, Y), eL = eager(X, Z);
-#endif
+    // compiler sees the candidate load consumed on every path.  T to 28 bytes, L to 12:
+    // L (the closer one) is taken when T is shorter than 12 and L at least as long,
+    // and C2 continues the taken candidate from where C1 stopped
+    // (tools/enc_model.c model4, pol 7 vs 0: ratio -0.1 %; measured -0.06 %, -3.4 % VALU).
+    const uint32_t eT = eager(X, Y);
+    const uint32_t eL = umin((first_diff_bit<2, 4>(X, Z) >> 3) + 4u, kEagerL);
     const uint32_t lT = okT ? eT : 0u, lL = okL ? eL : 0u;
-    const bool pickL = okL && (!okT || lL > lT || (lL == lT && cL > cT));
-#endif
+    const bool pickL = okL && (!okT || (lT < kEagerL && lL >= lT));
     R.c = pickL ? cL : cT;
     R.len = pickL ? lL : lT;
-    R.trunc1 = R.len >= kEagerLen && R.lim > kEagerLen;
+    R.base = pickL ? kEagerL : kEagerLen;
+    R.trunc1 = R.len >= R.base && R.lim > R.base;
     if (R.len > R.lim) R.len = R.lim;
     R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
     R.has = okT || okL;
     R.h = h;
-    load32<SMALL>(B.in, B.n, R.trunc1 ? (int)(R.c + kEagerLen) : 0, E,
+    load32<SMALL>(B.in, B.n, R.trunc1 ? (int)(R.c + R.base) : 0, E,
                   FAST || 64 * k + 123 <= B.n);
 }
 
@@ -414,11 +412,11 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
     bool trunc = false;
     {   // unconditional for the same reason as in C1
         uint32_t O[8];
-        ring32(S, p + kEagerLen, O);             // own bytes p+28 .. p+60
+        ring32(S, p + R.base, O);                // own bytes p+base .. p+base+32
         const uint32_t ext = umin(first_diff_bit<0, 8>(O, E) >> 3, 32u);
         if (R.trunc1) {
-            len = umin(kEagerLen + ext, R.lim);
-            trunc = ext == 32u && R.lim > kEager2;
+            len = umin(R.base + ext, R.lim);
+            trunc = ext == 32u && R.lim > R.base + 32u;
         }
     }
     uint32_t e2 = 0;

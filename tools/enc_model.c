@@ -215,6 +215,73 @@ static long model3(const uint8_t *in, int n, int hlog, int R, int lag, int sb, i
     return out;
 }
 
+
+/* Kernel policy (lz4_encode.hip): fixed 64-position chunks; the table lags `lag`
+ * chunks (walked positions + match_end - 2); L = earliest lane of the chunk with the
+ * same low `sb` hash bits; catch-up <= 4.  pol 0: T and L measured in full, longer
+ * wins (tie: closer); pol 7: L measured to 12 bytes only, taken when T is shorter
+ * than 12 and L at least as long (the product since the L-12 change). */
+static long model4(const uint8_t *in, int n, int lag, int pol, int sb)
+{
+    int tab[8192];
+    for (int i = 0; i < 8192; i++) tab[i] = -1;
+    int *cT = malloc(4 * n), *cL = malloc(4 * n), scr[256];
+    int *ins = malloc(8 * n), *insc = malloc(8 * n), nins = 0, done = 0;
+    const int mstart = n - 12, mlimit = n - 5, nch = (n + 63) / 64;
+    long out = 0;
+    int anchor = 0, p = 0;
+    g_hash = 1;
+    for (int k = 0; k < nch; k++) {
+        while (done < nins && insc[done] <= k - lag - 1) {
+            int q = ins[done++];
+            if (q + 8 <= n) tab[hsh(in + q, 13)] = q;
+        }
+        int r0 = 64 * k, r1 = r0 + 64 < n ? r0 + 64 : n;
+        for (int i = 0; i < (1 << sb); i++) scr[i] = -1;
+        for (int q = r0; q < r1; q++) {
+            uint32_t h = q + 8 <= n ? hsh(in + q, 13) : 0;
+            int s2 = h & ((1 << sb) - 1);
+            cT[q] = tab[h];
+            cL[q] = -1;
+            if (scr[s2] < 0) scr[s2] = q; else cL[q] = scr[s2];
+        }
+        while (p < r1) {
+            int best = 0, bc = -1;
+            if (p >= 1 && p <= mstart) {
+                int cs[2] = {cT[p], cL[p]}, ok[2], l[2] = {0, 0};
+                for (int j = 0; j < 2; j++) {
+                    int c = cs[j];
+                    ok[j] = !(c < 0 || c >= p || p - c > 65535) && rd32(in + c) == rd32(in + p);
+                    if (ok[j]) { l[j] = 4; while (p + l[j] < mlimit && in[p + l[j]] == in[c + l[j]]) l[j]++; }
+                }
+                int pick = -1;
+                if (pol == 7) {
+                    int l12 = l[1] < 12 ? l[1] : 12;
+                    if (ok[1] && (!ok[0] || (l[0] < 12 && l12 >= l[0]))) pick = 1;
+                    else if (ok[0]) pick = 0;
+                } else {
+                    if (ok[0]) pick = 0;
+                    if (ok[1] && (pick < 0 || l[1] >= l[0])) pick = 1;
+                }
+                if (pick >= 0) { best = l[pick]; bc = cs[pick]; }
+            }
+            ins[nins] = p; insc[nins++] = k;
+            if (best >= 4) {
+                int m = p, c = bc, len = best, b = 0;
+                while (b < 4 && m > anchor && c > 0 && in[m - 1] == in[c - 1]) { m--; c--; len++; b++; }
+                int lit = m - anchor;
+                out += 1 + ext(lit) + lit + 2 + ext(len - 4);
+                p = m + len;
+                anchor = p;
+                ins[nins] = p - 2; insc[nins++] = (p - 2) / 64 > k ? (p - 2) / 64 : k;
+            } else p++;
+        }
+    }
+    out += 1 + ext(n - anchor) + n - anchor;
+    free(cT); free(cL); free(ins); free(insc);
+    return out;
+}
+
 int main(int argc, char **argv)
 {
     const int n = 65536, nb = argc > 1 ? atoi(argv[1]) : 16;
@@ -264,6 +331,12 @@ int main(int argc, char **argv)
             tot += model3(buf + (size_t)b * n, n, T3[k].hlog, T3[k].R, T3[k].lag, T3[k].sb, T3[k].bcap);
         printf("prod/cons: hlog %d R %d lag %d scratch-bits %d back-cap %d       ratio %.4f\n", T3[k].hlog,
                T3[k].R, T3[k].lag, T3[k].sb, T3[k].bcap, (double)n * nb / tot);
+    }
+    for (int pol = 0; pol <= 7; pol += 7) {
+        long tot = 0;
+        for (int b = 0; b < nb; b++) tot += model4(buf + (size_t)b * n, n, 3, pol, 6);
+        printf("kernel policy: lag 3, L bits 6, pol %d                  ratio %.4f\n", pol,
+               (double)n * nb / tot);
     }
     free(buf);
     return 0;
