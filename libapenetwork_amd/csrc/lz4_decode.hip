@@ -370,52 +370,8 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
         if (full) bytes(std::false_type{}, std::true_type{});
         else bytes(std::false_type{}, std::false_type{});
     }
-    // in-step sources: follow them through the owner map (short chains, rare)
-    if (__any(pendm != 0)) {
-        uint32_t ow = 0, pr = pre;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            pr = umax(pr, (m >> (8 * j)) & 0xFFu);
-            ow |= pr << (8 * j);
-        }
-        wave_sync();
-        L.own[lane] = ow;
-        wave_sync();
-        while (__any(pendm != 0)) {
-            if (pendm) {
-                const int j0 = __builtin_ctz(pendm);
-                uint32_t x = pos[0];
-#pragma unroll
-                for (int j = 1; j < 4; j++)
-                    if (j == j0) x = pos[j];
-                const uint4 d = L.desc[((const uint8_t *)L.own)[x - base] - 1u];
-                const uint32_t le = d.y + d.z;
-                uint32_t na, nl = kNone, ng = 0;
-                bool still = false;
-                if (x < le) {
-                    na = d.x + (x - d.y);
-                    if (na - s0 < (uint32_t)kStage) nl = na - s0 + (uint32_t)offsetof(WaveLds, stage);
-                    else ng = 1;
-                } else if (d.w == 0) {
-                    na = 0;
-                } else {
-                    uint32_t k = x - le;
-                    if (k >= d.w) k %= d.w;
-                    na = le - d.w + k;
-                    if (DICT && na >= 0x80000000u) ng = 3;
-                    else if (na < gdone) ng = 2;
-                    else if (na < lo) nl = na & (kRing - 1);
-                    else still = true;
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if (j == j0) { pos[j] = na; lad[j] = nl; gk[j] = ng; }
-                anyg |= ng != 0u;
-                if (!still) pendm &= pendm - 1u;
-            }
-        }
-    }
-    // fetch: LDS for every byte, HBM only if a lane needs it
+    // fetch: LDS for every byte, HBM only if a lane needs it (an in-step source
+    // reads 0 here and is filled in below)
     const uint8_t *lds = (const uint8_t *)&L;
     uint32_t v[4];
 #pragma unroll
@@ -430,6 +386,60 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
             if (DICT && gk[j] == 3u) bp = D.dend - 0x100000000ll;   // dend + (int32)o
             const uint32_t g = __builtin_nontemporal_load(bp + o);
             v[j] = gk[j] != 0u ? g : v[j];
+        }
+    }
+    // In-step sources.  A pending byte's source (already reduced into the match's first
+    // period) is an earlier byte of this step.  The step's resolved bytes go to the
+    // ring, with a done flag per byte in the (no longer needed) owner map; each pass
+    // then copies every pending byte whose source is done.  Sources strictly precede
+    // their bytes, so each pass resolves at least the lowest pending byte of the step,
+    // and one pass usually resolves all.  No byte of this step reads the ring slots it
+    // overwrites (ring sources lie in [gdone, lo), and lo - gdone <= 512).
+#ifdef APE_DEXP_NOPEND
+    if (false) {   // diagnostic: instruction count without in-step sources (wrong bytes)
+#else
+    if (__any(pendm != 0)) {
+#endif
+        uint8_t *ring = L.ring;
+        uint8_t *done = (uint8_t *)L.own;
+        wave_sync();
+        uint32_t dw = 0;
+        if (lo == base && hi == base + kStep) {   // whole step: one dword (pending bytes 0)
+            *(uint32_t *)&ring[q0 & (kRing - 1)] = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t q = q0 + j;
+                if (q >= lo && q < hi) ring[q & (kRing - 1)] = (uint8_t)v[j];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) dw |= ((pendm >> j) & 1u) ? 0u : 1u << (8 * j);
+        L.own[lane] = dw;
+        wave_sync();
+        while (__any(pendm != 0)) {
+            uint32_t now = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t src = pos[j];
+                const bool pj = (pendm >> j) & 1u;
+                const uint32_t dn = done[pj ? src - base : 0u];
+                const uint32_t val = ring[src & (kRing - 1)];
+                const bool ok = pj && dn != 0u;
+                v[j] = ok ? val : v[j];
+                now |= ok ? 1u << j : 0u;
+            }
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if ((now >> j) & 1u) {
+                    const uint32_t q = q0 + j;
+                    ring[q & (kRing - 1)] = (uint8_t)v[j];
+                    done[q - base] = 1u;
+                }
+            }
+            pendm &= ~now;
+            wave_sync();
         }
     }
     const uint32_t word = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
