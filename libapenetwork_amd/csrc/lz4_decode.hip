@@ -285,7 +285,8 @@ __device__ __forceinline__ uint32_t reduce3(uint32_t x, uint32_t off) {
 // are guarded by wave-uniform tests only, so the wave does not juggle exec masks.
 template <bool DICT>
 __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t base, uint32_t lo,
-                                          uint32_t hi, uint32_t gdone, int nd, uint32_t d_out) {
+                                          uint32_t hi, uint32_t gdone, int nd, uint32_t d_out,
+                                          uint32_t &diag) {
     const int lane = D.lane;
     // owner map: mark descriptor starts inside (lo, hi); the one covering lo carries in
     const uint32_t cur = (uint32_t)__popcll(__ballot(lane < nd && d_out <= lo)) - 1u;
@@ -311,6 +312,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
     uint32_t rA = q0 - leA;                       // valid when q0 >= leA
     const bool needmod = q0 >= leA && offA != 0u && rA >= offA;
     if (__any(needmod)) {
+        diag |= 1u;
         if (needmod) rA %= offA;
     }
 
@@ -377,6 +379,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
 #pragma unroll
     for (int j = 0; j < 4; j++) v[j] = lds[lad[j]];   // kNone reads 0
     if (__any(anyg)) {
+        diag |= 0x10000u;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             // one nontemporal byte load for both sources (history in dst must bypass
@@ -400,6 +403,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
 #else
     if (__any(pendm != 0)) {
 #endif
+        diag |= 2u;
         uint8_t *ring = L.ring;
         uint8_t *done = (uint8_t *)L.own;
         wave_sync();
@@ -418,6 +422,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
         L.own[lane] = dw;
         wave_sync();
         while (__any(pendm != 0)) {
+            diag += 4u;
             uint32_t now = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -567,7 +572,13 @@ lz4_decode_kernel(BlockArgs a) {
                 gdone = lo;
             }
             wave_sync();
-            copy_step<DICT>(L, D, base, lo, hi, gdone, nd, d_out);
+            uint32_t diag = 0;
+            copy_step<DICT>(L, D, base, lo, hi, gdone, nd, d_out, diag);
+            STAT_ADD(5, diag & 1u);          // steps with a period division
+            STAT_ADD(6, (diag >> 1) & 1u);   // steps with in-step sources
+            STAT_ADD(7, (diag >> 2) & 0x3FFFu);   // their resolution passes
+            STAT_ADD(8, diag >> 16);         // steps reading HBM history / literals
+            (void)diag;
             STAT_ADD(3, 1);
         }
         cstart = cend;

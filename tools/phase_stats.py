@@ -13,8 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ.setdefault("APE_LZ4_LIB", os.path.join(ROOT, "libapenetwork_amd", "libape_lz4_amd_stats.so"))
 sys.path.insert(0, ROOT)
 
-DEC = ["parse", "copy", "(batches)", "(steps)", "(restages)", "", "", "", "", "", "(blocks)", "", "", "",
-       "", ""]
+DEC = ["parse", "copy", "(batches)", "(steps)", "(restages)", "(division steps)",
+       "(in-step source steps)", "(resolution passes)", "(HBM-read steps)", "", "(blocks)", "", "",
+       "", "", ""]
 ENC = ["W walk", "W publish", "E write", "W wait end", "W wait mid", "P A+B+C1",
        "P wait mid", "P C2", "P wait end", "", "(steps x3 waves)", "(members)", "E prepare",
        "(blocks)", "E wait mid", "E wait end"]
