@@ -487,20 +487,24 @@ struct WalkOut {
     uint64_t walked, members;
     uint32_t m_back, m_len, an;   // per member lane
     uint2 iv;
+    uint32_t q0, Lf;              // walk start; forward match length per lane
 };
 
-__device__ __forceinline__ void walk_chunk(const EncLds &S, const Blk &B, int k, int lane, Walk &W,
+// First half: the hop chain only (the latency-bound part); second half, before the
+// inserts: the lane-parallel catch-up limits, walked set and anchor (walk_finish).
+__device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k, int lane, Walk &W,
                                            WalkOut &O) {
     const uint32_t P = 64u * (uint32_t)k;
     O.walked = O.members = 0;
     O.m_back = O.m_len = O.an = 0;
     O.iv = S.info[k % 3][lane];
+    O.q0 = W.q;
+    O.Lf = O.iv.x & 0xFFu;                               // forward match length
     if (W.q >= P + 64u) return;               // a match from earlier chunks covers it
     const uint2 iv = O.iv;
     const bool has = (iv.x & I_HAS) != 0u, trunc = (iv.x & I_TRUNC) != 0u;
-    uint32_t Lf = iv.x & 0xFFu;                          // forward match length
     const uint64_t Hm = __ballot(has);
-    const uint32_t Lh = has ? (trunc ? 0x80u : Lf) : 0u;   // hop; 0x80 = unfinished
+    const uint32_t Lh = has ? (trunc ? 0x80u : O.Lf) : 0u;   // hop; 0x80 = unfinished
     uint32_t rel = W.q - P;
     uint64_t M = 0;
     for (;;) {
@@ -513,29 +517,34 @@ __device__ __forceinline__ void walk_chunk(const EncLds &S, const Blk &B, int k,
             const uint32_t me = P + j;
             const uint32_t cm = me - (lane_val(iv.y, (int)j) & 0xFFFFu);
             const uint32_t Le = extend_match(B, me, cm, lane_val(iv.x, (int)j) & 0xFFu, lane);
-            if ((uint32_t)lane == j) Lf = Le;
+            if ((uint32_t)lane == j) O.Lf = Le;
             rel = j + Le;
         } else {
             rel = j + h;
         }
         if (rel >= 64u) break;
     }
+    O.members = M;
+    W.q = P + rel;
+}
+
+__device__ __forceinline__ void walk_finish(int k, int lane, Walk &W, WalkOut &O) {
+    const uint32_t P = 64u * (uint32_t)k;
+    if (O.q0 >= P + 64u) return;              // covered by a match from earlier chunks
     // catch-up limits: a member's backward extension stops at the previous end
     const uint32_t anchor0 = W.anchor;
-    const bool mem = (M >> lane) & 1ull;
+    const bool mem = (O.members >> lane) & 1ull;
     const uint32_t p = P + (uint32_t)lane;
-    const uint32_t end = mem ? p + Lf : 0u;
+    const uint32_t end = mem ? p + O.Lf : 0u;
     const uint32_t imax = wave_incl_max(end);
     const uint32_t pm = umax(wave_shr1(imax, 0u), anchor0);
-    const uint32_t bk = umin((iv.x >> 8) & 7u, p - pm);
-    O.members = M;
+    const uint32_t bk = umin((O.iv.x >> 8) & 7u, p - pm);
     O.m_back = bk;
-    O.m_len = Lf + bk;
+    O.m_len = O.Lf + bk;
     O.an = pm;
     // walked = every position from the walk start that no match of this chunk covers
-    O.walked = __ballot(p >= W.q && pm <= p);
+    O.walked = __ballot(p >= O.q0 && pm <= p);
     W.anchor = umax(anchor0, lane_val(imax, 63));
-    W.q = P + rel;
 }
 
 __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int lane,
@@ -794,11 +803,12 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         __syncthreads();
         for (int s = k0; s < nsteps; s++) {
             const bool work = s >= k0 + 1 && s <= nch;
-            if (work) walk_chunk(S, B, s - 1, lane, W, O);
+            if (work) walk_chain(S, B, s - 1, lane, W, O);
             STAT(0);
             __syncthreads();
             STAT(4);
             if (work) {
+                walk_finish(s - 1, lane, W, O);
                 walk_publish(S, B, s - 1, lane, O);
                 STAT_ADD(11, __popcll(O.members));
             }
