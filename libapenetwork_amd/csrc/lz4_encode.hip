@@ -227,8 +227,10 @@ __device__ __forceinline__ uint32_t div255(uint32_t e) {
     return (uint32_t)__umul24(e, 0x8081u) >> 23;
 }
 
-__device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {  // bytes after a 15 nibble
-    return v >= 15 ? div255(v - 15) + 1 : 0;
+// bytes after a 15 nibble: v < 15 -> 0, else (v - 15) / 255 + 1 -- both are
+// (v + 240) / 255 (v + 240 < 255 below 15; one full-rate multiply, no select)
+__device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {
+    return div255(v + 240u);
 }
 
 // write the length extension of v (>= 15) at o
@@ -674,14 +676,14 @@ __device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int kA, int 
         // every candidate value computed, then selected (no divergent branches)
         const uint32_t rr = b - r_ex;                    // offset inside the sequence
         const uint32_t rml = r_mo & 0xFFFFu, roff = r_mo >> 16;
-        const uint32_t el = rl - 15u, fl = div255(el);   // literal-length extension
-        const uint32_t lit_at = 1u + (rl >= 15u ? fl + 1u : 0u), off_at = lit_at + rl;
-        const uint32_t em = rml - 15u, fm = div255(em);  // match-length extension
+        const uint32_t lit_at = 1u + ext_bytes(rl), off_at = lit_at + rl;
         const uint32_t a = r_an + (rr - lit_at);         // literal source position
         uint32_t v = ((const uint8_t *)S.ring)[a & (kRingE - 1)];
         if (rr >= lit_at && rr < off_at && a < rlo) v = B.in[a];   // older than the ring (rare)
-        const uint32_t vl = (rr - 1u < fl) ? 255u : el - 255u * fl;
-        const uint32_t vm = (rr - off_at - 2u < fm) ? 255u : em - 255u * fm;
+        // length extension bytes: 255 while more than 254 remain, then the rest
+        // (the i-th byte after the nibble is min(255, v - 15 - 255 i))
+        const uint32_t vl = umin(rl - 15u - (uint32_t)__umul24(rr - 1u, 255u), 255u);
+        const uint32_t vm = umin(rml - 15u - (uint32_t)__umul24(rr - off_at - 2u, 255u), 255u);
         const uint32_t vo = rr == off_at ? (roff & 0xFFu) : (roff >> 8);
         v = rr < off_at ? v : (rr < off_at + 2u ? vo : vm);
         v = rr < lit_at ? vl : v;
@@ -840,15 +842,26 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         const bool work = true;
 #endif
         const int r = s - k0;
+#ifdef APE_EMIT_SINGLE
+        if (work && E.pend && E.kA == s - 3) {   // diagnostic: one chunk per write
+            emit_write(S, B, s - 3, lane, E);
+            E.pend = false;
+        }
+#else
         if (work && E.pend && E.kA == s - 4) {   // the pair prepared in steps s-2, s-1
             emit_write(S, B, s - 4, lane, E);
             E.pend = false;
         }
+#endif
         STAT(2);
         __syncthreads();
         STAT(14);
         if (work && r >= 2 && s - 2 < nch) {
+#ifdef APE_EMIT_SINGLE
+            if (true) {
+#else
             if (((r - 2) & 1) == 0) {            // first chunk of a pair
+#endif
                 E.Bc.members = 0;
                 E.Bc.tot = 0;
                 emit_prepare(S, B, s - 2, lane, E, E.A, 0u);
