@@ -244,7 +244,7 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const bool bad = fin ? badfin : stop;
     const int rv = fin ? (badfin ? -ipl - 1 : (int)cpy)
                        : ((e_off || mlerr) ? -ipo - 1 : -q - 1);
-    const uint64_t sm = __ballot(mem && stop) & M;
+    const uint64_t sm = wave_ballot(mem && stop) & M;
     uint64_t emit = M;
     int st = ST_MORE;
     if (sm) {
@@ -289,10 +289,10 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
                                           uint32_t &diag) {
     const int lane = D.lane;
     // owner map: mark descriptor starts inside (lo, hi); the one covering lo carries in
-    const uint32_t cur = (uint32_t)__popcll(__ballot(lane < nd && d_out <= lo)) - 1u;
+    const uint32_t cur = (uint32_t)__popcll(wave_ballot(d_out <= lo)) - 1u;   // d_out = ~0 past nd
     L.own[lane] = 0u;
     wave_sync();
-    if (lane < nd && d_out > lo && d_out < hi) ((uint8_t *)L.own)[d_out - base] = (uint8_t)(lane + 1);
+    if (d_out - lo - 1u < hi - lo - 1u) ((uint8_t *)L.own)[d_out - base] = (uint8_t)(lane + 1);  // lo < d_out < hi
     wave_sync();
     const uint32_t m = L.own[lane];
     const uint32_t run = umax(umax(m & 0xFFu, (m >> 8) & 0xFFu), umax((m >> 16) & 0xFFu, m >> 24));
@@ -311,7 +311,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
     // offset of byte 0 inside A's match period (one division, only if some lane needs it)
     uint32_t rA = q0 - leA;                       // valid when q0 >= leA
     const bool needmod = q0 >= leA && offA != 0u && rA >= offA;
-    if (__any(needmod)) {
+    if (wave_any(needmod)) {
         diag |= 1u;
         if (needmod) rA %= offA;
     }
@@ -365,7 +365,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
     };
     const bool so = offA - 1u < 3u || offB - 1u < 3u;
     const bool full = lo == base && hi == base + kStep;
-    if (__any(so)) {
+    if (wave_any(so)) {
         if (full) bytes(std::true_type{}, std::true_type{});
         else bytes(std::true_type{}, std::false_type{});
     } else {
@@ -378,7 +378,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
     uint32_t v[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) v[j] = lds[lad[j]];   // kNone reads 0
-    if (__any(anyg)) {
+    if (wave_any(anyg)) {
         diag |= 0x10000u;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -401,7 +401,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
 #ifdef APE_DEXP_NOPEND
     if (false) {   // diagnostic: instruction count without in-step sources (wrong bytes)
 #else
-    if (__any(pendm != 0)) {
+    if (wave_any(pendm != 0)) {
 #endif
         diag |= 2u;
         uint8_t *ring = L.ring;
@@ -421,7 +421,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
         for (int j = 0; j < 4; j++) dw |= ((pendm >> j) & 1u) ? 0u : 1u << (8 * j);
         L.own[lane] = dw;
         wave_sync();
-        while (__any(pendm != 0)) {
+        while (wave_any(pendm != 0)) {
             diag += 4u;
             uint32_t now = 0;
 #pragma unroll
@@ -550,13 +550,13 @@ lz4_decode_kernel(BlockArgs a) {
         // ---- COPY the batch's output [cstart, cend) ----
         wave_sync();
         const uint32_t bend = op;
-        const uint32_t d_out = lane < nd ? L.desc[lane].y : 0u;
+        const uint32_t d_out = lane < nd ? L.desc[lane].y : 0xFFFFFFFFu;   // ~0 past nd
         // Copy through the last step boundary and carry the descriptors from the
         // owner of that boundary on; with no new boundary, carry them all.  The
         // last batch, or one that would carry too many, copies through its end.
         uint32_t cend = bend & ~(uint32_t)(kStep - 1);
         int keep = 0;
-        if (cend > cstart) keep = __popcll(__ballot(lane < nd && d_out <= cend)) - 1;
+        if (cend > cstart) keep = __popcll(wave_ballot(d_out <= cend)) - 1;
         else cend = cstart;
         const bool carry = st == ST_MORE && cend < bend && nd - keep <= kMaxCarry;
         if (!carry) cend = bend;

@@ -466,7 +466,7 @@ __device__ __forceinline__ uint32_t extend_match(const Blk &B, uint32_t m, uint3
                 if (e) { d = 1; at = 4u * (uint32_t)t + (__builtin_ctz(e) >> 3); }
             }
         }
-        const uint64_t bad = __ballot(d != 0 || kk >= lm);
+        const uint64_t bad = wave_ballot(d != 0 || kk >= lm);
         if (bad) {
             const int fl = __builtin_ctzll(bad);
             const uint32_t k2 = L + 16u * (uint32_t)fl;
@@ -505,7 +505,7 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     if (W.q >= P + 64u) return;               // a match from earlier chunks covers it
     const uint2 iv = O.iv;
     const bool has = (iv.x & I_HAS) != 0u, trunc = (iv.x & I_TRUNC) != 0u;
-    const uint64_t Hm = __ballot(has);
+    const uint64_t Hm = wave_ballot(has);
     const uint32_t Lh = has ? (trunc ? 0x80u : O.Lf) : 0u;   // hop; 0x80 = unfinished
     uint32_t rel = W.q - P;
     uint64_t M = 0;
@@ -545,7 +545,7 @@ __device__ __forceinline__ void walk_finish(int k, int lane, Walk &W, WalkOut &O
     O.m_len = O.Lf + bk;
     O.an = pm;
     // walked = every position from the walk start that no match of this chunk covers
-    O.walked = __ballot(p >= O.q0 && pm <= p);
+    O.walked = wave_ballot(p >= umax(O.q0, pm));
     W.anchor = umax(anchor0, lane_val(imax, 63));
 }
 
@@ -642,10 +642,12 @@ __device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int kA, int 
     const uint32_t rlo = P + 448u > kRingE ? P + 448u - kRingE : 0u;
     const bool memA = (E.A.members >> lane) & 1ull, memB = (E.Bc.members >> lane) & 1ull;
     const uint32_t exA = E.A.ex, exB = totA + E.Bc.ex;
+    // member starts, ~0 for other lanes: the window tests below are single compares
+    const uint32_t sA = memA ? exA : 0xFFFFFFFFu, sB = memB ? exB : 0xFFFFFFFFu;
     gu8 *out = B.dst + E.o;
     for (uint32_t w = 0; w < tot; w += 64u) {
-        const bool markA = memA && exA > w && exA < w + 64u;
-        const bool markB = memB && exB > w && exB < w + 64u;
+        const bool markA = sA - w - 1u < 63u;    // w < start < w + 64
+        const bool markB = sB - w - 1u < 63u;
         if (markA) ((uint8_t *)S.omap)[exA - w] = (uint8_t)(lane + 1);
         if (markB) ((uint8_t *)S.omap)[exB - w] = (uint8_t)(lane + 65);
         __builtin_amdgcn_sched_barrier(0);
@@ -653,8 +655,8 @@ __device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int kA, int 
         __builtin_amdgcn_sched_barrier(0);
         if (markA) ((uint8_t *)S.omap)[exA - w] = 0;
         if (markB) ((uint8_t *)S.omap)[exB - w] = 0;
-        const uint64_t covA = __ballot(memA && exA <= w);   // member 0 of A starts at 0
-        const uint64_t covB = __ballot(memB && exB <= w);
+        const uint64_t covA = wave_ballot(sA <= w);   // member 0 of A starts at 0
+        const uint64_t covB = wave_ballot(sB <= w);
         const uint32_t carry = covB ? 128u - (uint32_t)__clzll((long long)covB)
                                     : 64u - (uint32_t)__clzll((long long)covA);
         const uint32_t own = umax(wave_incl_max(mk), carry) - 1u;

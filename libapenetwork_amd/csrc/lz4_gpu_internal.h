@@ -46,6 +46,11 @@ __device__ __forceinline__ void gstore4(gu8 *p, uint32_t v) {
 // ---- wave64 helpers ----
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
+// Wave votes on a bool: HIP's __ballot / __any take an int, and the int round trip
+// costs a v_cndmask + v_cmp per vote where the condition already is a lane mask.
+__device__ __forceinline__ uint64_t wave_ballot(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+__device__ __forceinline__ bool wave_any(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
+
 // DPP lane moves (GFX9-family controls, available on gfx950): lanes whose
 // source is outside the row / masked off keep `old`.
 template <int CTRL, int ROW_MASK = 0xF>
