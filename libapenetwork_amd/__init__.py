@@ -17,7 +17,7 @@ __all__ = [
     "decompress_safe", "decompress_safe_partial", "compress_batch", "decompress_batch",
     "decompress_partial_batch", "synth_blocks", "gpu_init", "gpu_last_error", "GpuError",
     "MAX_BLOCK", "ERANGE", "frame_offsets", "frame_pack", "decompress_frames",
-    "compress_prefix_batch", "decompress_dict_batch",
+    "compress_prefix_batch", "decompress_dict_batch", "compress_fast_ptr_batch",
 ]
 
 _HERE = _os.path.dirname(_os.path.abspath(__file__))
@@ -54,6 +54,7 @@ def lib():
             "APE_LZ4_gpu_device_count": (i, []),
             "APE_LZ4_gpu_last_error": (cp, []),
             "APE_LZ4_compress_batch_dev": (i, [p, p, p, p, p, i, p]),
+            "APE_LZ4_compress_fast_batch_dev": (i, [p, p, p, p, p, i, i, p]),
             "APE_LZ4_decompress_safe_batch_dev": (i, [p, p, p, p, p, i, p]),
             "APE_LZ4_decompress_safe_partial_batch_dev": (i, [p, p, p, p, p, p, i, p]),
             "APE_LZ4_compress_batch_strided_dev": (i, [p, sz, p, p, sz, p, p, i, p]),
@@ -167,6 +168,15 @@ def decompress_partial_batch(src_ptrs, comp_sizes, dst_ptrs, targets, caps, resu
     _check(lib().APE_LZ4_decompress_safe_partial_batch_dev(
         _ptr(src_ptrs), _ptr(comp_sizes), _ptr(dst_ptrs), _ptr(targets), _ptr(caps),
         _ptr(results), n, _stream(stream)), "APE_LZ4_decompress_safe_partial_batch_dev")
+
+
+def compress_fast_ptr_batch(src_ptrs, src_sizes, dst_ptrs, caps, results, acceleration,
+                            stream=None):
+    """N x APE_LZ4_compress_fast, pointer-array form (int64 tensors of pointers)."""
+    n = src_sizes.shape[0]
+    _check(lib().APE_LZ4_compress_fast_batch_dev(
+        _ptr(src_ptrs), _ptr(src_sizes), _ptr(dst_ptrs), _ptr(caps), _ptr(results), n,
+        acceleration, _stream(stream)), "APE_LZ4_compress_fast_batch_dev")
 
 
 def decompress_ptr_batch(src_ptrs, comp_sizes, dst_ptrs, caps, results, stream=None):

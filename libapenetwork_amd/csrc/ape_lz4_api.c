@@ -37,11 +37,11 @@ static void gpu_failed(int rt)
     }
 }
 
-static int gpu_compress(const char *src, char *dst, int n, int cap)
+static int gpu_compress(const char *src, char *dst, int n, int cap, int accel)
 {
     int rt = 0, r;
     if ((unsigned)n > (unsigned)LZ4_MAX_INPUT_SIZE) return 0; /* ref :558 */
-    r = ape_lz4_gpu_compress_one(src, dst, n, cap, &rt);
+    r = ape_lz4_gpu_compress_one(src, dst, n, cap, accel, &rt);
     if (rt) { gpu_failed(rt); return 0; }
     if (r == APE_LZ4_GPU_ERANGE) {
         fprintf(stderr, "libape_lz4_amd: block of %d bytes exceeds the GPU block limit (%d)\n",
@@ -65,14 +65,15 @@ int APE_LZ4_sizeofState(void) { return LZ4_STREAMSIZE; }
 /* ---- one-shot compression (ref :758-836, :1679-1699) -> GPU ---- */
 int APE_LZ4_compress_default(const char *source, char *dest, int inputSize, int maxOutputSize)
 {
-    return gpu_compress(source, dest, inputSize, maxOutputSize);
+    return gpu_compress(source, dest, inputSize, maxOutputSize, 1);
 }
 
 int APE_LZ4_compress_fast(const char *source, char *dest, int inputSize, int maxOutputSize,
                           int acceleration)
 {
-    (void)acceleration; /* the GPU parse has no skip heuristic to accelerate */
-    return gpu_compress(source, dest, inputSize, maxOutputSize);
+    /* > 1 trades ratio for speed, as in the reference (:789-808); the GPU parse has no
+       skip heuristic, so it drops the in-chunk candidate instead */
+    return gpu_compress(source, dest, inputSize, maxOutputSize, acceleration);
 }
 
 int APE_LZ4_compress_fast_extState(void *state, const char *source, char *dest, int inputSize,

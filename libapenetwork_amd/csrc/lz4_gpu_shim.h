@@ -6,7 +6,7 @@
 #if defined(__cplusplus)
 extern "C" {
 #endif
-int ape_lz4_gpu_compress_one(const char *src, char *dst, int n, int cap, int *rt);
+int ape_lz4_gpu_compress_one(const char *src, char *dst, int n, int cap, int accel, int *rt);
 int ape_lz4_gpu_decompress_one(const char *src, char *dst, int csize, int cap, int partial,
                                int target, int *rt);
 #if defined(__cplusplus)

@@ -113,7 +113,7 @@ inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
 // Staging layout (same offsets on host and device):
 //   [ptr arrays: src, dst][int arrays: in_size, cap, target, result][inputs][outputs]
 // mode: 0 = compress, 1 = decompress_safe, 2 = decompress_safe_partial
-int host_batch(int mode, const char *const *h_src, const int *h_in, char *const *h_dst,
+int host_batch(int mode, int accel, const char *const *h_src, const int *h_in, char *const *h_dst,
                const int *h_cap, const int *h_target, int *h_res, int nb) {
     if (nb < 0 || (nb > 0 && (!h_src || !h_in || !h_dst || !h_cap || !h_res))) {
         snprintf(g_err, sizeof g_err, "invalid argument");
@@ -165,6 +165,7 @@ int host_batch(int mode, const char *const *h_src, const int *h_in, char *const 
     hipError_t e = hipMemcpyAsync(D, H, out_off[0], hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return finish_launch(e, "hipMemcpyAsync H2D");
     BlockArgs a{};
+    a.accel = accel;
     a.src = (const char *const *)D;
     a.dst = (char *const *)(D + (size_t)nb * sizeof(void *));
     a.src_size = (const int *)(D + ioff);
@@ -227,6 +228,18 @@ int APE_LZ4_compress_batch_dev(const char *const *d_src, const int *d_srcSize,
                                                 d_result, nblocks),
                                        (hipStream_t)stream),
                          "lz4_encode_kernel");
+}
+
+int APE_LZ4_compress_fast_batch_dev(const char *const *d_src, const int *d_srcSize,
+                                    char *const *d_dst, const int *d_dstCap, int *d_result,
+                                    int nblocks, int acceleration, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_srcSize || !d_dst || !d_dstCap || !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    BlockArgs a = ptr_args(d_src, d_srcSize, d_dst, d_dstCap, nullptr, d_result, nblocks);
+    a.accel = acceleration;
+    return finish_launch(launch_encode(a, (hipStream_t)stream), "lz4_encode_kernel");
 }
 
 int APE_LZ4_decompress_safe_batch_dev(const char *const *d_src, const int *d_compressedSize,
@@ -385,13 +398,13 @@ int APE_LZ4_decompress_safe_frames_dev(const char *d_frames, const long long *d_
 int APE_LZ4_compress_batch_host(const char *const *h_src, const int *h_srcSize,
                                 char *const *h_dst, const int *h_dstCap, int *h_result,
                                 int nblocks) {
-    return host_batch(0, h_src, h_srcSize, h_dst, h_dstCap, nullptr, h_result, nblocks);
+    return host_batch(0, 1, h_src, h_srcSize, h_dst, h_dstCap, nullptr, h_result, nblocks);
 }
 
 int APE_LZ4_decompress_safe_batch_host(const char *const *h_src, const int *h_compressedSize,
                                        char *const *h_dst, const int *h_maxDecompressedSize,
                                        int *h_result, int nblocks) {
-    return host_batch(1, h_src, h_compressedSize, h_dst, h_maxDecompressedSize, nullptr,
+    return host_batch(1, 1, h_src, h_compressedSize, h_dst, h_maxDecompressedSize, nullptr,
                       h_result, nblocks);
 }
 
@@ -422,16 +435,16 @@ int APE_LZ4_debug_stats(int which, unsigned long long *out16, int reset) {
 #endif
 
 // ---- internal shim for the one-shot C API (ape_lz4_api.c) ----
-int ape_lz4_gpu_compress_one(const char *src, char *dst, int n, int cap, int *rt) {
+int ape_lz4_gpu_compress_one(const char *src, char *dst, int n, int cap, int accel, int *rt) {
     int res = 0;
-    *rt = host_batch(0, &src, &n, &dst, &cap, nullptr, &res, 1);
+    *rt = host_batch(0, accel, &src, &n, &dst, &cap, nullptr, &res, 1);
     return res;
 }
 
 int ape_lz4_gpu_decompress_one(const char *src, char *dst, int csize, int cap, int partial,
                                int target, int *rt) {
     int res = 0;
-    *rt = host_batch(partial ? 2 : 1, &src, &csize, &dst, &cap, partial ? &target : nullptr,
+    *rt = host_batch(partial ? 2 : 1, 1, &src, &csize, &dst, &cap, partial ? &target : nullptr,
                      &res, 1);
     return res;
 }

@@ -40,7 +40,12 @@ def test_one_shot_compress_roundtrip(cuda, product, oracle):
         assert L.APE_LZ4_compress(buf(src), o, len(src)) == r
         st = C.create_string_buffer(16416)
         assert L.APE_LZ4_compress_withState(st, buf(src), o, len(src)) == r
-        assert L.APE_LZ4_compress_fast_extState(st, buf(src), o, len(src), len(comp), 5) == r
+        assert L.APE_LZ4_compress_fast_extState(st, buf(src), o, len(src), len(comp), 1) == r
+        # acceleration > 1 trades ratio for speed (ref :789-808): still a valid block
+        fo = C.create_string_buffer(product.compressBound(len(src)) + 16)
+        fr = L.APE_LZ4_compress_fast_extState(st, buf(src), fo, len(src),
+                                              product.compressBound(len(src)), 5)
+        assert fr > 0 and orc_decompress(oracle, fo.raw[:fr], len(src)) == (len(src), src)
         if r > 1:
             assert L.APE_LZ4_compress_limitedOutput(buf(src), o, len(src), r - 1) == 0
 

@@ -110,3 +110,34 @@ def test_pathological_runs(cuda, product, oracle):
 def test_block_limit(cuda, product):
     rs, _ = run_encode(cuda, product, [bytes(65537)])
     assert rs == [product.ERANGE]
+
+
+def test_acceleration(cuda, product, oracle):
+    """compress_fast with acceleration > 1 (ref src/ape_lz4.c:789-808): valid blocks at a
+    lower ratio; acceleration <= 1 is compress_default's output byte for byte."""
+    srcs = [I.synth_comp(65536, b) for b in range(32)] + \
+           [I.make(c, n, seed=n) for c in ("text", "zeros", "rand", "period3")
+            for n in (0, 13, 100, 4096, 65536)]
+    src, sptr, _ = pack(cuda, srcs)
+    caps = [product.compressBound(len(s)) for s in srcs]
+    out = {}
+    for accel in (1, 2, 8):
+        dst, dptr, doffs = alloc_out(cuda, caps)
+        res = ints(cuda, [0] * len(srcs))
+        sizes, capt = ints(cuda, map(len, srcs)), ints(cuda, caps)
+        product.compress_fast_ptr_batch(sptr, sizes, dptr, capt, res, accel)
+        cuda.cuda.synchronize()
+        rs = res.cpu().tolist()
+        out[accel] = (rs, [fetch(dst, o, r) for o, r in zip(doffs, rs)])
+        for s, c in zip(srcs, out[accel][1]):
+            check_valid(oracle, s, c)
+    rs1, comps1 = run_encode(cuda, product, srcs)
+    assert out[1][1] == comps1
+    assert out[2][1] == out[8][1]
+    fast = 32 * 65536 / sum(out[2][0][:32])
+    dflt = 32 * 65536 / sum(rs1[:32])
+    print("ratio default %.4f accelerated %.4f" % (dflt, fast))
+    assert 0.95 * dflt <= fast <= dflt
+    # the one-shot API routes acceleration too
+    r, c = product.compress_fast(srcs[0], acceleration=4)
+    assert c == out[2][1][0]
