@@ -103,6 +103,15 @@ int APE_LZ4_decompress_safe_usingDict_batch_dev(const char *const *d_src,
                                                 const char *const *d_dict, const int *d_dictSize,
                                                 int *d_result, int nblocks, void *stream);
 
+/* == N x APE_LZ4_decompress_fast(src, dst, originalSize) (ref src/ape_lz4.c:1489):
+ * d_result[i] <- compressed bytes consumed, or -(consumed)-1.  The reference reads its
+ * input without a bound; the batch needs d_srcBound[i] = the readable bytes at d_src[i]
+ * (e.g. compressBound(originalSize)), and rejects an offset reaching before d_dst[i]
+ * (the reference reads memory before dst there). */
+int APE_LZ4_decompress_fast_batch_dev(const char *const *d_src, const int *d_srcBound,
+                                      char *const *d_dst, const int *d_originalSize,
+                                      int *d_result, int nblocks, void *stream);
+
 /* ---- batched, device-resident, strided form (block i at base + i*stride) ----
  * The layout the benchmark uses: uncompressed slots of `src_stride` bytes,
  * compressed slots of `dst_stride` bytes; a NULL cap array means

@@ -134,7 +134,10 @@ enum { ST_MORE = 0, ST_DONE = 1, ST_ERR = 2 };
 // Scalar restatement of one iteration of the reference loop (:1324-1458) for a
 // token at ip: appends its descriptor at desc[nd] (returns ST_MORE / ST_DONE) or
 // reports the error (ST_ERR); `res` gets the block result when not ST_MORE.
-template <bool PARTIAL>
+// FASTD: decompress_fast (endOnOutputSize, :1489): the block ends where the output
+// reaches cap exactly; no input-size tests (csize is only the readable bound of src);
+// the result is the input consumed.
+template <bool PARTIAL, bool FASTD = false>
 __device__ int parse_scalar(WaveLds &L, const Dec &D, int &ip, uint32_t &op, int &nd, int &res) {
     const uint32_t tok = sbyte(L, D.src, D.csize, D.s0, ip);
     ip++;
@@ -145,19 +148,21 @@ __device__ int parse_scalar(WaveLds &L, const Dec &D, int &ip, uint32_t &op, int
             s = sbyte(L, D.src, D.csize, D.s0, ip);
             ip++;
             lit += s;
-        } while (ip < D.csize - 15 && s == 255);
+        } while ((FASTD || ip < D.csize - 15) && s == 255);
     }
     const int64_t cpy = (int64_t)op + lit;  // :1345-1370
-    const bool fin = (PARTIAL ? (cpy > D.oexit) : (cpy > (int64_t)D.cap - kMFLimit)) ||
-                     ((int64_t)ip + lit > (int64_t)D.csize - 8);
+    const bool fin = FASTD ? (cpy > (int64_t)D.cap - 8)   // WILDCOPYLENGTH
+                           : ((PARTIAL ? (cpy > D.oexit) : (cpy > (int64_t)D.cap - kMFLimit)) ||
+                              ((int64_t)ip + lit > (int64_t)D.csize - 8));
     if (fin) {
-        const bool bad = PARTIAL ? (cpy > D.cap || (int64_t)ip + lit > D.csize)
-                                 : ((int64_t)ip + lit != D.csize || cpy > D.cap);
+        const bool bad = FASTD ? (cpy != D.cap)
+                               : (PARTIAL ? (cpy > D.cap || (int64_t)ip + lit > D.csize)
+                                          : ((int64_t)ip + lit != D.csize || cpy > D.cap));
         if (bad) { res = -ip - 1; return ST_ERR; }
         if (D.lane == 0) L.desc[nd] = make_uint4((uint32_t)ip, op, (uint32_t)lit, 0u);
         nd++;
         op = (uint32_t)cpy;
-        res = (int)cpy;
+        res = FASTD ? ip + (int)lit : (int)cpy;
         return ST_DONE;
     }
     const int lit_src = ip;
@@ -171,7 +176,7 @@ __device__ int parse_scalar(WaveLds &L, const Dec &D, int &ip, uint32_t &op, int
     if (ml == 15) {
         uint32_t s;
         do {
-            if (ip > D.csize - kLastLiterals) { res = -ip - 1; return ST_ERR; }
+            if (!FASTD && ip > D.csize - kLastLiterals) { res = -ip - 1; return ST_ERR; }
             s = sbyte(L, D.src, D.csize, D.s0, ip);
             ip++;
             ml += s;
@@ -188,7 +193,7 @@ __device__ int parse_scalar(WaveLds &L, const Dec &D, int &ip, uint32_t &op, int
 // One speculative window at P (P - s0 + kWinNeed <= kStage): appends the
 // chain's descriptors.  Returns ST_MORE with P advanced (to the next token, or
 // to a complex token when `cplx`), or ST_DONE / ST_ERR with `res`.
-template <bool PARTIAL, bool DICT>
+template <bool PARTIAL, bool DICT, bool FASTD = false>
 __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int &nd, int &res,
                             bool &cplx) {
     const int lane = D.lane;
@@ -203,9 +208,9 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const int p = P + lane;
     const int ipl = p + 1;                       // first literal byte
     const int ipo = ipl + (int)lit + 2;          // after the offset
-    const bool fin_in = (uint32_t)ipl + lit + 8u > (uint32_t)D.csize;   // ipl >= 1, csize > 0
+    const bool fin_in = !FASTD && (uint32_t)ipl + lit + 8u > (uint32_t)D.csize;   // ipl >= 1
     const bool mlx = mn == 15u;
-    const bool mlerr = mlx && ipo + kLastLiterals > D.csize;
+    const bool mlerr = !FASTD && mlx && ipo + kLastLiterals > D.csize;
     const bool cx = lit == 15u || (mlx && e == 255u && !mlerr);
     const uint32_t ml = mlx ? 15u + e : mn;
     const int q = ipo + (mlx ? 1 : 0);           // next token
@@ -235,14 +240,19 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     // token has lit < 15 and ml < 274, and op + ex stays far below 2^32.
     const uint32_t cpy = opl + lit, ucap = (uint32_t)D.cap;
     const uint32_t iend = (uint32_t)ipl + lit;  // input position after the literals
-    const bool fin = fin_in || (PARTIAL ? ((int64_t)cpy > D.oexit) : (cpy + (uint32_t)kMFLimit > ucap));
-    const bool badfin = PARTIAL ? (cpy > ucap || iend > (uint32_t)D.csize)
-                                : (iend != (uint32_t)D.csize || cpy > ucap);
+    // FASTD (:1346-1366 with endOnOutputSize): final once the literals pass cap - 8,
+    // valid only when they end exactly at cap; the result is the input consumed
+    const bool fin = FASTD ? (cpy + 8u > ucap)
+                           : (fin_in || (PARTIAL ? ((int64_t)cpy > D.oexit)
+                                                 : (cpy + (uint32_t)kMFLimit > ucap)));
+    const bool badfin = FASTD ? (cpy != ucap)
+                              : (PARTIAL ? (cpy > ucap || iend > (uint32_t)D.csize)
+                                         : (iend != (uint32_t)D.csize || cpy > ucap));
     const bool e_off = (DICT ? cpy + D.dsz : cpy) < off;               // :1375-1376
     const bool e_cap = cpy + ml + (uint32_t)(kMinMatch + kLastLiterals) > ucap;   // :1444
     const bool stop = fin || e_off || mlerr || e_cap;
     const bool bad = fin ? badfin : stop;
-    const int rv = fin ? (badfin ? -ipl - 1 : (int)cpy)
+    const int rv = fin ? (badfin ? -ipl - 1 : (int)(FASTD ? iend : cpy))
                        : ((e_off || mlerr) ? -ipo - 1 : -q - 1);
     const uint64_t sm = wave_ballot(mem && stop) & M;
     uint64_t emit = M;
@@ -266,7 +276,8 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
         nd += __popcll(emit);
         if (emit) {
             const int last = 63 - __clzll((long long)emit);
-            op = lane_val(opl + ob, last);
+            // (FASTD: a final sequence's size is its literals; ob assumed a match)
+            op = lane_val(opl + ((FASTD && fin) ? lit : ob), last);
         }
     }
     if (st == ST_MORE) P += (int)c;
@@ -473,7 +484,7 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
 
 }  // namespace
 
-template <bool PARTIAL, bool DICT>
+template <bool PARTIAL, bool DICT, bool FASTD>
 __global__ void __launch_bounds__(64)
 lz4_decode_kernel(BlockArgs a) {
     __shared__ WaveLds L;
@@ -505,6 +516,10 @@ lz4_decode_kernel(BlockArgs a) {
 
     // Special cases of :1316-1318 and the empty-input quirk (the reference reads
     // src[0] even when compressedSize <= 0).
+    if (FASTD && (D.cap == 0 || D.csize <= 0)) {   // :1321-1322 (and no readable input)
+        if (lane == 0) a.result[b] = (D.cap == 0 && D.csize > 0 && D.src[0] == 0) ? 1 : -1;
+        return;
+    }
     if (D.cap == 0 || D.csize <= 0) {
         if (lane == 0) {
             int r;
@@ -538,9 +553,9 @@ lz4_decode_kernel(BlockArgs a) {
         while (st == ST_MORE && nd <= kFlushAt) {
             if (P - D.s0 + kWinNeed > kStage) { restage = true; break; }
             bool cplx;
-            st = parse_window<PARTIAL, DICT>(L, D, P, op, nd, result, cplx);
+            st = parse_window<PARTIAL, DICT, FASTD>(L, D, P, op, nd, result, cplx);
             if (st == ST_MORE && cplx) {
-                st = parse_scalar<PARTIAL>(L, D, P, op, nd, result);
+                st = parse_scalar<PARTIAL, FASTD>(L, D, P, op, nd, result);
                 // a complex token may jump far past the staged bytes
                 if (st == ST_MORE && P - D.s0 + kWinNeed > kStage) { restage = true; break; }
             }
@@ -608,12 +623,14 @@ lz4_decode_kernel(BlockArgs a) {
 
 hipError_t launch_decode(const BlockArgs &a, bool partial, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
-    if (a.dict)   // usingDict decodes are full decodes (ref :1625-1647)
-        hipLaunchKernelGGL((lz4_decode_kernel<false, true>), dim3(a.nblocks), dim3(64), 0, s, a);
+    if (a.fast)   // decompress_fast (ref :1489)
+        hipLaunchKernelGGL((lz4_decode_kernel<false, false, true>), dim3(a.nblocks), dim3(64), 0, s, a);
+    else if (a.dict)   // usingDict decodes are full decodes (ref :1625-1647)
+        hipLaunchKernelGGL((lz4_decode_kernel<false, true, false>), dim3(a.nblocks), dim3(64), 0, s, a);
     else if (partial)
-        hipLaunchKernelGGL((lz4_decode_kernel<true, false>), dim3(a.nblocks), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((lz4_decode_kernel<true, false, false>), dim3(a.nblocks), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((lz4_decode_kernel<false, false>), dim3(a.nblocks), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((lz4_decode_kernel<false, false, false>), dim3(a.nblocks), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -131,6 +131,7 @@ struct BlockArgs {
                                  // (frame i = [le32 size][block] at src_base + frame_off[i])
     const char *const *dict;  // decoder: per-block external dictionary (nullable) ...
     const int *dict_size;     // ... and its size (usingDict, ref src/ape_lz4.c:1625-1647)
+    int fast;                 // decoder: decompress_fast (src_size = readable bound of src)
     int accel;                // encoder: acceleration (compress_fast, :789); > 1 drops the
                               // in-chunk candidate (faster, lower ratio)
     int *result;

@@ -293,6 +293,19 @@ int APE_LZ4_decompress_safe_usingDict_batch_dev(const char *const *d_src,
                          "lz4_decode_kernel<usingDict>");
 }
 
+int APE_LZ4_decompress_fast_batch_dev(const char *const *d_src, const int *d_srcBound,
+                                      char *const *d_dst, const int *d_originalSize,
+                                      int *d_result, int nblocks, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_srcBound || !d_dst || !d_originalSize ||
+                                         !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    BlockArgs a = ptr_args(d_src, d_srcBound, d_dst, d_originalSize, nullptr, d_result, nblocks);
+    a.fast = 1;
+    return finish_launch(launch_decode(a, false, (hipStream_t)stream), "lz4_decode_kernel<fast>");
+}
+
 int APE_LZ4_compress_withPrefix_batch_dev(const char *const *d_src, const int *d_srcSize,
                                           const int *d_prefixSize, char *const *d_dst,
                                           const int *d_dstCap, int *d_result, int nblocks,

@@ -126,8 +126,16 @@ def main():
             # round-trip decode KATs at cap = n, n - 1, n + 7
             if n <= 8192:
                 for cap in sorted({n, max(n - 1, 0), n + 7}):
-                    fx["decode"].append(dec_case("rt_%s_%d_cap%d" % (content, n, cap), comp,
-                                                 cap, rng))
+                    case = dec_case("rt_%s_%d_cap%d" % (content, n, cap), comp, cap, rng)
+                    # decompress_fast (:1489) with originalSize = cap <= n: the reference
+                    # stays inside the stream (a larger size would read past it)
+                    if cap <= n:
+                        fo = C.create_string_buffer(max(cap, 1) + 64)
+                        fr = F("decompress_fast")(cbuf(comp), fo, cap)
+                        case["fast"] = {"osize": cap, "ret": fr}
+                        if fr > 0:
+                            case["fast"]["out_sha256"] = I.sha(fo.raw[:cap])
+                    fx["decode"].append(case)
     # 2. crafted malformed streams (App. D.2)
     crafted = {
         "empty_src_cap8_tok00": (b"", 8),

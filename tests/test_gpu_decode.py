@@ -143,3 +143,63 @@ def test_strided_batch_benchmark_layout(cuda, product, oracle):
     host = out.cpu().numpy()
     for b in range(nb):
         assert host[b].tobytes() == srcs[b]
+
+
+def test_decompress_fast(cuda, product, oracle):
+    """decompress_fast (ref src/ape_lz4.c:1489): consumed bytes and output identical to the
+    oracle on valid blocks with the exact original size, and the same error code when the
+    size is short (the reference then stops inside the stream)."""
+    import ctypes as C
+    from lz4util import buf
+    srcs = [I.make(c, n, seed=n) for c in ("comp", "text", "zeros", "rand", "period3")
+            for n in (13, 14, 100, 300, 4096, 65536)]
+    srcs += [I.synth_comp(65536, b) for b in range(8)]
+    comps = [orc_compress(oracle, s)[1] for s in srcs]
+    # the GPU encoder's blocks too
+    src_t, sptr, _ = pack(cuda, srcs)
+    caps0 = [product.compressBound(len(s)) for s in srcs]
+    dst0, dptr0, doffs0 = alloc_out(cuda, caps0)
+    res0 = ints(cuda, [0] * len(srcs))
+    sizes0, capt0 = ints(cuda, map(len, srcs)), ints(cuda, caps0)
+    product.compress_fast_ptr_batch(sptr, sizes0, dptr0, capt0, res0, 1)
+    cuda.cuda.synchronize()
+    comps += [fetch(dst0, o, r) for o, r in zip(doffs0, res0.cpu().tolist())]
+    plains = srcs + srcs
+    cases = []   # (comp, original size)
+    for c, s in zip(comps, plains):
+        cases.append((c, len(s)))
+        for k in (1, 3, 8, 13, 100):
+            if len(s) - k >= 0:
+                cases.append((c, len(s) - k))
+    blobs = [c for c, _ in cases]
+    ins, iptr, _ = pack(cuda, blobs)
+    osz = [n for _, n in cases]
+    dst, dptr, doffs = alloc_out(cuda, [max(n, 1) for n in osz])
+    res = ints(cuda, [0] * len(cases))
+    product.decompress_fast_ptr_batch(iptr, ints(cuda, [len(b) for b in blobs]), dptr,
+                                      ints(cuda, osz), res)
+    cuda.cuda.synchronize()
+    rs = res.cpu().tolist()
+    for i, (c, n) in enumerate(cases):
+        o = C.create_string_buffer(max(n, 1) + 64)
+        er = oracle.orc_decompress_fast(buf(c), o, n)
+        assert rs[i] == er, (i, n, len(c), rs[i], er)
+        if er > 0:
+            assert fetch(dst, doffs[i], n) == o.raw[:n], i
+
+
+def test_decompress_fast_golden(cuda, product, golden):
+    """The reference's own decompress_fast results (tests/golden, originalSize = n, n - 1)."""
+    cases = [d for d in golden["decode"] if "fast" in d]
+    comps = [base64.b64decode(d["comp_b64"]) for d in cases]
+    ins, iptr, _ = pack(cuda, comps)
+    osz = [d["fast"]["osize"] for d in cases]
+    dst, dptr, doffs = alloc_out(cuda, [max(n, 1) for n in osz])
+    res = ints(cuda, [0] * len(cases))
+    product.decompress_fast_ptr_batch(iptr, ints(cuda, [len(c) for c in comps]), dptr,
+                                      ints(cuda, osz), res)
+    cuda.cuda.synchronize()
+    for i, (d, r) in enumerate(zip(cases, res.cpu().tolist())):
+        assert r == d["fast"]["ret"], d["name"]
+        if r > 0:
+            assert I.sha(fetch(dst, doffs[i], osz[i])) == d["fast"]["out_sha256"], d["name"]

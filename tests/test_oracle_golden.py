@@ -48,6 +48,23 @@ def test_decode_kats(oracle, golden):
             assert sha(pout) == p["out_sha256"], d["name"]
 
 
+def test_decode_fast_kats(oracle, golden):
+    """decompress_fast (ref :1489) on the reference's own results (valid streams,
+    originalSize = n and n - 1)."""
+    n = 0
+    for d in golden["decode"]:
+        if "fast" not in d:
+            continue
+        comp, f = base64.b64decode(d["comp_b64"]), d["fast"]
+        out = C.create_string_buffer(max(f["osize"], 1) + 64)
+        r = oracle.orc_decompress_fast(buf(comp), out, f["osize"])
+        assert r == f["ret"], d["name"]
+        if r > 0:
+            assert sha(out.raw[:f["osize"]]) == f["out_sha256"], d["name"]
+        n += 1
+    assert n > 200
+
+
 @pytest.mark.parametrize("idx", [0, 1, 2])
 def test_stream_kats(oracle, golden, idx):
     st = golden["stream"][idx]
