@@ -151,6 +151,7 @@ __device__ int parse_scalar(WaveLds &L, const Dec &D, int &ip, uint32_t &op, int
         } while ((FASTD || ip < D.csize - 15) && s == 255);
     }
     const int64_t cpy = (int64_t)op + lit;  // :1345-1370
+    if (FASTD && (int64_t)ip + lit > D.csize) { res = -ip - 1; return ST_ERR; }  // bound
     const bool fin = FASTD ? (cpy > (int64_t)D.cap - 8)   // WILDCOPYLENGTH
                            : ((PARTIAL ? (cpy > D.oexit) : (cpy > (int64_t)D.cap - kMFLimit)) ||
                               ((int64_t)ip + lit > (int64_t)D.csize - 8));
@@ -167,6 +168,7 @@ __device__ int parse_scalar(WaveLds &L, const Dec &D, int &ip, uint32_t &op, int
     }
     const int lit_src = ip;
     ip += (int)lit;
+    if (FASTD && ip + 2 > D.csize) { res = -ip - 1; return ST_ERR; }   // bound
     const uint32_t off = sbyte(L, D.src, D.csize, D.s0, ip) |
                          (sbyte(L, D.src, D.csize, D.s0, ip + 1) << 8);  // :1373-1376
     ip += 2;
@@ -249,10 +251,14 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
                               : (PARTIAL ? (cpy > ucap || iend > (uint32_t)D.csize)
                                          : (iend != (uint32_t)D.csize || cpy > ucap));
     const bool e_off = (DICT ? cpy + D.dsz : cpy) < off;               // :1375-1376
+    // FASTD: the bytes a sequence needs must lie inside the readable bound (the reference
+    // has no bound and reads on; here that is an error, never a read past the buffer)
+    const bool e_in = FASTD && (fin ? iend > (uint32_t)D.csize
+                                    : (uint32_t)q > (uint32_t)D.csize);
     const bool e_cap = cpy + ml + (uint32_t)(kMinMatch + kLastLiterals) > ucap;   // :1444
-    const bool stop = fin || e_off || mlerr || e_cap;
-    const bool bad = fin ? badfin : stop;
-    const int rv = fin ? (badfin ? -ipl - 1 : (int)(FASTD ? iend : cpy))
+    const bool stop = fin || e_off || mlerr || e_cap || e_in;
+    const bool bad = fin ? (badfin || e_in) : stop;
+    const int rv = fin ? ((badfin || e_in) ? -ipl - 1 : (int)(FASTD ? iend : cpy))
                        : ((e_off || mlerr) ? -ipo - 1 : -q - 1);
     const uint64_t sm = wave_ballot(mem && stop) & M;
     uint64_t emit = M;

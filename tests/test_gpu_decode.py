@@ -203,3 +203,32 @@ def test_decompress_fast_golden(cuda, product, golden):
         assert r == d["fast"]["ret"], d["name"]
         if r > 0:
             assert I.sha(fetch(dst, doffs[i], osz[i])) == d["fast"]["out_sha256"], d["name"]
+
+
+def test_decompress_fast_garbage_stays_in_bounds(cuda, product, oracle):
+    """decompress_fast on mutated and random inputs: the reference reads on without a bound
+    (undefined there); the batch must stay inside each source's readable bound and dst,
+    and return either an error or at most the bound."""
+    rng = random.Random(17)
+    blobs, osz = [], []
+    for k in range(600):
+        n = rng.choice([16, 100, 1000, 4096, 65536])
+        c = bytearray(orc_compress(oracle, I.make(rng.choice(["comp", "text", "zeros"]), n,
+                                                  seed=k))[1])
+        for _ in range(rng.randint(1, 6)):
+            c[rng.randrange(len(c))] = rng.randrange(256)
+        if rng.random() < 0.3:
+            c = c[:rng.randrange(1, len(c) + 1)]
+        blobs.append(bytes(c))
+        osz.append(n + rng.choice([0, 0, -3, 7, 300]))
+    for k in range(100):
+        blobs.append(bytes(rng.randrange(256) for _ in range(rng.randrange(1, 600))))
+        osz.append(rng.randrange(1, 5000))
+    ins, iptr, _ = pack(cuda, blobs, extra=0)
+    dst, dptr, doffs = alloc_out(cuda, osz)
+    res = ints(cuda, [0] * len(blobs))
+    product.decompress_fast_ptr_batch(iptr, ints(cuda, [len(b) for b in blobs]), dptr,
+                                      ints(cuda, osz), res)
+    cuda.cuda.synchronize()
+    for b, r in zip(blobs, res.cpu().tolist()):
+        assert r <= len(b)
