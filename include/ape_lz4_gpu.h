@@ -112,6 +112,19 @@ int APE_LZ4_decompress_fast_batch_dev(const char *const *d_src, const int *d_src
                                       char *const *d_dst, const int *d_originalSize,
                                       int *d_result, int nblocks, void *stream);
 
+/* == N x APE_LZ4_compress_destSize(src, dst, &srcSize, targetDstSize) (ref
+ * src/ape_lz4.c:1048-1067, :843-1021): d_srcSize[i] is in/out -- on entry the input size,
+ * on return the input bytes the block encodes; d_result[i] <- bytes written to d_dst[i]
+ * (<= d_targetDstSize[i]; 0 if the target is < 1 or the size negative).  The output is a
+ * valid LZ4 block of src[0, consumed) (decodes with cap = consumed); when the whole block
+ * fits the target it is compress_default's output.  Bytes and consumed size differ from
+ * the reference's greedy cut (the GPU parse is chunk-parallel; the cut is at a sequence
+ * boundary followed by as many literals as fit).  Uses stream-ordered scratch of
+ * ~65.8 KB per block, at most 16384 blocks at a time. */
+int APE_LZ4_compress_destSize_batch_dev(const char *const *d_src, int *d_srcSize,
+                                        char *const *d_dst, const int *d_targetDstSize,
+                                        int *d_result, int nblocks, void *stream);
+
 /* ---- batched, device-resident, strided form (block i at base + i*stride) ----
  * The layout the benchmark uses: uncompressed slots of `src_stride` bytes,
  * compressed slots of `dst_stride` bytes; a NULL cap array means

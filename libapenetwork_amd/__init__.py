@@ -18,7 +18,7 @@ __all__ = [
     "decompress_partial_batch", "synth_blocks", "gpu_init", "gpu_last_error", "GpuError",
     "MAX_BLOCK", "ERANGE", "frame_offsets", "frame_pack", "decompress_frames",
     "compress_prefix_batch", "decompress_dict_batch", "compress_fast_ptr_batch",
-    "decompress_fast_ptr_batch",
+    "decompress_fast_ptr_batch", "compress_destSize_ptr_batch",
 ]
 
 _HERE = _os.path.dirname(_os.path.abspath(__file__))
@@ -56,6 +56,7 @@ def lib():
             "APE_LZ4_gpu_last_error": (cp, []),
             "APE_LZ4_compress_batch_dev": (i, [p, p, p, p, p, i, p]),
             "APE_LZ4_compress_fast_batch_dev": (i, [p, p, p, p, p, i, i, p]),
+            "APE_LZ4_compress_destSize_batch_dev": (i, [p, p, p, p, p, i, p]),
             "APE_LZ4_decompress_fast_batch_dev": (i, [p, p, p, p, p, i, p]),
             "APE_LZ4_decompress_safe_batch_dev": (i, [p, p, p, p, p, i, p]),
             "APE_LZ4_decompress_safe_partial_batch_dev": (i, [p, p, p, p, p, p, i, p]),
@@ -179,6 +180,15 @@ def compress_fast_ptr_batch(src_ptrs, src_sizes, dst_ptrs, caps, results, accele
     _check(lib().APE_LZ4_compress_fast_batch_dev(
         _ptr(src_ptrs), _ptr(src_sizes), _ptr(dst_ptrs), _ptr(caps), _ptr(results), n,
         acceleration, _stream(stream)), "APE_LZ4_compress_fast_batch_dev")
+
+
+def compress_destSize_ptr_batch(src_ptrs, src_sizes, dst_ptrs, targets, results, stream=None):
+    """N x APE_LZ4_compress_destSize, pointer-array form: src_sizes (int32) is in/out --
+    input sizes on entry, consumed input bytes on return; results = bytes written."""
+    n = src_sizes.shape[0]
+    _check(lib().APE_LZ4_compress_destSize_batch_dev(
+        _ptr(src_ptrs), _ptr(src_sizes), _ptr(dst_ptrs), _ptr(targets), _ptr(results), n,
+        _stream(stream)), "APE_LZ4_compress_destSize_batch_dev")
 
 
 def decompress_fast_ptr_batch(src_ptrs, src_bounds, dst_ptrs, original_sizes, results,

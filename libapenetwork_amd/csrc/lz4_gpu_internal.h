@@ -140,6 +140,11 @@ struct BlockArgs {
 
 hipError_t launch_decode(const BlockArgs &a, bool partial, hipStream_t s);
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s);
+// compress_destSize pass 2 (lz4_destsize.hip): scratch slot i (at scratch + i*stride, encoder
+// result sres[i]) -> dst[i] cut to target[i]; src_size[i] <- consumed input
+hipError_t launch_destsize(const char *const *src, int *src_size, char *const *dst,
+                           const int *target, int *result, const char *scratch, size_t stride,
+                           const int *sres, int n, hipStream_t s);
 hipError_t launch_frame_offsets(const int *csize, long long *off, long long *scratch, int n,
                                 hipStream_t s);
 int frame_scratch_elems(int n);

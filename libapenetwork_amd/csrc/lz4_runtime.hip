@@ -320,6 +320,47 @@ int APE_LZ4_compress_withPrefix_batch_dev(const char *const *d_src, const int *d
     return finish_launch(launch_encode(a, (hipStream_t)stream), "lz4_encode_kernel<prefix>");
 }
 
+int APE_LZ4_compress_destSize_batch_dev(const char *const *d_src, int *d_srcSize,
+                                        char *const *d_dst, const int *d_targetDstSize,
+                                        int *d_result, int nblocks, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_srcSize || !d_dst || !d_targetDstSize ||
+                                         !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    if (nblocks == 0) return APE_LZ4_GPU_OK;
+    // scratch: full-size encoder output for up to kSub blocks at a time, stream-ordered
+    // (allocated and freed on the caller's stream, so concurrent calls never share it)
+    constexpr int kSub = 16384;
+    const size_t stride = up16((size_t)kMaxBlock + kMaxBlock / 255 + 16);
+    const int sub = nblocks < kSub ? nblocks : kSub;
+    hipStream_t s = (hipStream_t)stream;
+    char *scr = nullptr;
+    hipError_t e = hipMallocAsync((void **)&scr, (size_t)sub * stride + (size_t)sub * sizeof(int), s);
+    if (e != hipSuccess) {
+        set_err("hipMallocAsync (destSize scratch)", e);
+        return APE_LZ4_GPU_ENOMEM;
+    }
+    int *sres = (int *)(scr + (size_t)sub * stride);
+    for (int off = 0; off < nblocks && e == hipSuccess; off += sub) {
+        const int m = nblocks - off < sub ? nblocks - off : sub;
+        BlockArgs a{};
+        a.src = d_src + off;
+        a.dst_base = scr;
+        a.dst_stride = stride;  // cap = stride >= compressBound: every block fits
+        a.src_size = d_srcSize + off;
+        a.result = sres;
+        a.nblocks = m;
+        e = launch_encode(a, s);
+        if (e == hipSuccess)
+            e = launch_destsize(d_src + off, d_srcSize + off, d_dst + off, d_targetDstSize + off,
+                                d_result + off, scr, stride, sres, m, s);
+    }
+    hipError_t ef = hipFreeAsync(scr, s);
+    if (e == hipSuccess) e = ef;
+    return finish_launch(e, "lz4_encode_kernel + lz4_destsize_kernel");
+}
+
 int APE_LZ4_compress_batch_strided_dev(const char *d_src, size_t src_stride, const int *d_srcSize,
                                        char *d_dst, size_t dst_stride, const int *d_dstCap,
                                        int *d_result, int nblocks, void *stream) {

@@ -141,3 +141,56 @@ def test_acceleration(cuda, product, oracle):
     # the one-shot API routes acceleration too
     r, c = product.compress_fast(srcs[0], acceleration=4)
     assert c == out[2][1][0]
+
+
+def test_destsize(cuda, product, oracle):
+    """compress_destSize batched on the GPU (ref src/ape_lz4.c:843-1067): the output fits
+    the target, decodes (oracle decompress_safe, cap = consumed) to exactly the consumed
+    prefix, is compress_default's output when the block fits, and consumes about as much
+    input as the reference's greedy cut (reported; aggregate >= 95 % of it for targets of
+    at least 1000 bytes)."""
+    import ctypes as C
+
+    from lz4util import buf
+
+    base = [I.synth_comp(65536, b) for b in range(6)] + \
+           [I.make(c, n, seed=n) for c in ("text", "zeros", "rand", "period3")
+            for n in (0, 1, 13, 100, 4096, 65536)]
+    full_rs, full = run_encode(cuda, product, base)
+    srcs, tgts = [], []
+    for s, c in zip(base, full_rs):
+        for t in (0, 1, 2, 10, 16, 17, 100, 1000, 5000, 20000, c - 1, c, c + 7,
+                  product.compressBound(len(s))):
+            srcs.append(s)
+            tgts.append(t)
+    src, sptr, _ = pack(cuda, srcs)
+    dst, dptr, doffs = alloc_out(cuda, [max(t, 0) for t in tgts])
+    sizes, tg = ints(cuda, map(len, srcs)), ints(cuda, tgts)
+    res = ints(cuda, [-7] * len(srcs))
+    product.compress_destSize_ptr_batch(sptr, sizes, dptr, tg, res)
+    cuda.cuda.synchronize()
+    rs, cons = res.cpu().tolist(), sizes.cpu().tolist()
+    gpu_sum = ref_sum = 0
+    full_by = {id(s): f for s, f in zip(base, full)}
+    for i, (s, t) in enumerate(zip(srcs, tgts)):
+        r, k = rs[i], cons[i]
+        if t < 1:
+            assert r == 0 and k == len(s), (i, t, r, k)
+            continue
+        assert 1 <= r <= t and 0 <= k <= len(s), (i, len(s), t, r, k)
+        comp = fetch(dst, doffs[i], r)
+        dr, out = orc_decompress(oracle, comp, k)
+        assert dr == k and out == s[:k], (i, len(s), t, r, k, dr)
+        walk_ok(comp)
+        if t >= len(full_by[id(s)]):
+            assert k == len(s) and comp == full_by[id(s)], (i, t)
+        rsz = C.c_int(len(s))
+        rd = C.create_string_buffer(t + 64)
+        rr = oracle.orc_compress_destSize(buf(s), rd, C.byref(rsz), t)
+        assert rr > 0
+        if t >= 1000:
+            gpu_sum += k
+            ref_sum += rsz.value
+    print("destSize consumed: GPU %d vs reference %d (%.4f)" % (gpu_sum, ref_sum,
+                                                               gpu_sum / ref_sum))
+    assert gpu_sum >= 0.95 * ref_sum
