@@ -1,29 +1,32 @@
 #!/usr/bin/env python3
 """bench.py -- LZ4 GiB/s device-resident (compress+decompress), 1M x 64 KiB blocks.
 
-BASELINE.json metric / config 3 ("1M x 64 KiB compressible blocks, compress+decompress,
-1 MI355X"); with --gpus N under torch.distributed.run every rank processes its own
-1M-block shard (distinct blocks: block ids rank*N .. ), no collective on the data
-path, and the reported value is the whole-job aggregate (weak scaling).
+BASELINE.json metric / configs 3 and 4: 1,048,576 x 64 KiB compressible blocks,
+compress+decompress.  With --gpus N under torch.distributed.run the fixed batch is split
+contiguously (rank r takes blocks [r*N_total/N, (r+1)*N_total/N), 131072 per GPU at N = 8;
+strong scaling, "scaling": "strong"), with no collective on the data path: a gloo process
+group carries the barrier, the max-over-ranks time and the per-rank numbers (`per_gpu`).
+--weak gives every rank its own 1M blocks instead.
 
-One step = compress every block (one launch of lz4_encode_kernel over all blocks)
-then decompress every compressed block (one launch of lz4_decode_kernel); inputs are
-generated on the device before timing (SURVEY App. C `gen_comp`, seed = block id).
-value = uncompressed bytes of all ranks / max-over-ranks step time.  Correctness is
-checked after timing (every decoded block == its source, sampled GPU-compressed blocks
-restored by the oracle = the reference decoder restated), and the compression ratio
-is reported beside the throughput.
+One step = compress every block of the rank (one launch of lz4_encode_kernel) then
+decompress every compressed block (one launch of lz4_decode_kernel); inputs are generated
+on the device before timing (SURVEY App. C `gen_comp`, seed = block id).  value =
+uncompressed bytes of the job / max-over-ranks step time.  Correctness is checked after
+timing (every decoded block == its source; sampled GPU-compressed blocks restored by the
+oracle = the reference decoder restated) and the compression ratio is reported.
 
-roofline: the dominant kernel's algorithmic bytes (encode: n + c per block, decode:
-c + n) per launch / its average duration from HIP events on the launch stream.
-cpu_baseline: the reference src/ape_lz4.c (oracle/_ref, built from the reference
-sources) -- or the oracle restatement if absent -- timed on this host's cores over a
-bounded sample of the same workload, rank 0 at N=1 only.
+Also in the line (rank 0, N = 1): `config2` = BASELINE config 2 (256K x 4 KiB random blocks
+compressed by the reference algorithm, decode only) with its own roofline and CPU baseline;
+`cpu_baseline` = the reference src/ape_lz4.c built from its own source with gcc and clang
+(oracle/_ref), a 1..N thread sweep over the box's usable cores on a 4 GiB sample;
+`roofline` = the dominant kernel's algorithmic bytes / its HIP-event time, plus the
+decoder's and the whole step's fractions and the HBM-read roofline the north_star names.
 """
 import argparse
 import ctypes as C
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -41,66 +44,146 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(block, kind, target_s):
-    """Reference codec on host cores, compress_default + decompress_safe per block."""
+def host_cores():
+    """Usable host cores of this box and how they were determined (BASELINE.md section 4:
+    state nproc / lscpu).  usable = the affinity mask, capped by a cgroup CPU quota and by
+    OMP_NUM_THREADS when the harness sets it as the job's CPU share (the GPU box exposes the
+    whole machine's CPUs to os.cpu_count() but grants one GPU job a share of them)."""
+    info = {"os_cpu_count": os.cpu_count()}
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    info["affinity"] = aff
+    usable = aff
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = round(int(q) / int(per), 2)
+            usable = min(usable, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp:
+        info["OMP_NUM_THREADS"] = omp
+        if omp < usable:
+            usable = omp
+            info["limited_by"] = "OMP_NUM_THREADS (the job's CPU share on this box)"
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    if model is None:
+        try:
+            for line in open("/proc/cpuinfo"):
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            pass
+    info["model"] = model
+    info["usable"] = usable
+    return usable, info
+
+
+def _ref_libs():
+    """(label, path, symbol prefix, kind) of the CPU codecs to time: the reference
+    compiled from its own source with gcc and with clang (oracle/_ref, BASELINE.md
+    section 4), else the oracle restatement."""
+    libs = []
+    for label, name in (("gcc", "libape_lz4_ref.so"), ("clang", "libape_lz4_ref_clang.so")):
+        p = os.path.join(ROOT, "oracle", "_ref", name)
+        if os.path.exists(p):
+            libs.append((label, p, b"APE_LZ4_", "reference"))
+    if not libs:
+        libs.append(("gcc", os.path.join(ROOT, "oracle", "liblz4_oracle.so"), b"orc_", "port"))
+    return libs
+
+
+def _cpubench():
     lib = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
-    lib.cpu_bench_run.restype = C.c_int
-    lib.cpu_bench_run.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int,
-                                  C.c_int, C.POINTER(C.c_double)]
-    ref = os.path.join(ROOT, "oracle", "_ref", "libape_lz4_ref.so")
-    if os.path.exists(ref):
-        path, prefix, kindname = ref, b"APE_LZ4_", "reference"
-    else:
-        path, prefix, kindname = os.path.join(ROOT, "oracle", "liblz4_oracle.so"), b"orc_", "port"
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    lib.cpu_bench_prepare.restype = C.c_void_p
+    lib.cpu_bench_prepare.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int]
+    lib.cpu_bench_time.restype = C.c_int
+    lib.cpu_bench_time.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    lib.cpu_bench_free.argtypes = [C.c_void_p]
+    return lib
+
+
+def _sweep_threads(usable):
+    ts, t = [], 1
+    while t < usable:
+        ts.append(t)
+        t *= 2
+    return ts + [usable]
+
+
+def cpu_baseline(block, kind, nblocks, mode=0):
+    """The reference codec on this host's cores: one block per
+    task, static partition, a 1..N thread sweep, gcc and clang builds.  mode 0 =
+    compress_default + decompress_safe (config 3), 1 = decompress_safe only (config 2).
+    The sample is generated and compressed once untimed; each sweep point times one
+    full pass over it (after a warm-up pass) and checks every decoded block."""
+    usable, cores = host_cores()
+    lib = _cpubench()
     out = (C.c_double * 5)()
-    # calibrate on a small sample, then size the sample for ~target_s of wall time
-    nb = 1024
-    rc = lib.cpu_bench_run(path.encode(), prefix, threads, nb, block, kind, 1, out)
-    if rc != 0:
-        return None
-    per_block = (out[0] + out[1]) / nb
-    nb = int(min(32768, max(1024, target_s / max(per_block, 1e-9) / 2)))
-    reps = max(1, int(target_s / max(per_block * nb, 1e-9)))
-    rc = lib.cpu_bench_run(path.encode(), prefix, threads, nb, block, kind, reps, out)
-    if rc != 0 or out[3] != 0:
-        return None
-    tc, td, csz, bytes_ = out[0], out[1], out[2], out[4]
-    return {
-        "value": round(bytes_ * reps / (tc + td) / GIB, 3),
-        "unit": "GiB/s",
-        "cores": threads,
-        "kind": kindname,
-        "sample": "%d x %d KiB %s blocks x %d reps, compress_default + decompress_safe, "
-                  "%d threads (static block partition), %.1f s" % (
-                      nb, block >> 10, "compressible" if kind else "random", reps, threads,
-                      tc + td),
-        "compress_GiBps": round(bytes_ * reps / tc / GIB, 3),
-        "decompress_GiBps": round(bytes_ * reps / td / GIB, 3),
-        "ratio": round(bytes_ / csz, 4),
+    sweep, best, split, kindname = [], None, {}, None
+    threads = _sweep_threads(usable)
+    for label, path, prefix, kname in _ref_libs():
+        kindname = kname
+        h = lib.cpu_bench_prepare(path.encode(), prefix, nblocks, block, kind, usable)
+        if not h:
+            return None
+        try:
+            for t in threads:
+                if lib.cpu_bench_time(h, t, 1, mode, out) != 0 or out[3] != 0:
+                    return None
+                tc, td, csz, byt = out[0], out[1], out[2], out[4]
+                v = byt / (tc + td) / GIB
+                row = next((r for r in sweep if r["threads"] == t), None)
+                if row is None:
+                    row = {"threads": t}
+                    sweep.append(row)
+                row[label] = round(v, 3)
+                if t == usable:
+                    split[label] = {"value": round(v, 3),
+                                    "decompress_GiBps": round(byt / td / GIB, 3),
+                                    "ratio": round(byt / csz, 4)}
+                    if mode == 0:
+                        split[label]["compress_GiBps"] = round(byt / tc / GIB, 3)
+                    if best is None or v > best[1]:
+                        best = (label, v)
+        finally:
+            lib.cpu_bench_free(h)
+    label, v = best
+    what = ("compress_default + decompress_safe" if mode == 0 else "decompress_safe only")
+    res = {
+        "value": round(v, 3), "unit": "GiB/s", "cores": usable, "kind": kindname,
+        "compiler": label,
+        "sample": "%d x %d KiB %s blocks (%.2f GiB), %s, one block per task, static partition "
+                  "over %d threads; best of %s at %d threads" % (
+                      nblocks, block >> 10, "compressible" if kind else "random",
+                      nblocks * block / GIB, what, usable, "/".join(split), usable),
+        "host": cores, "sweep": sweep, "by_compiler": split,
     }
+    res.update({k: v2 for k, v2 in split[label].items() if k != "value"})
+    return res
 
 
 def pmc_traffic(kernel, blocks):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass, scaled per block."""
+    """HBM bytes per launch, PROFILE-DERIVED: FETCH_SIZE (x2, gfx950) + WRITE_SIZE per block
+    from the committed rocprofv3 --pmc passes (profiles/pmc_traffic.json), times the blocks
+    of this launch -- not measured by this run."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))[kernel]
-        return int(d["bytes_per_block"] * blocks)
+        return int(d["bytes_per_block"] * blocks), d.get("source", "profiles/pmc_traffic.json")
     except Exception:
-        return None
-
-
-def sq_issue(kernel):
-    """VALU-pipe occupancy of `kernel` from the committed SQ PMC passes (tools/sq_issue.py):
-    the binding resource of this integer byte-shuffling path is instruction issue, not HBM."""
-    p = os.path.join(ROOT, "profiles", "sq_issue.json")
-    try:
-        d = json.load(open(p))[kernel]
-        return {"pipe": "valu", "busy": d["valu_pipe_busy"], "salu_busy": d["salu_busy"],
-                "source": "profiles/sq_issue.json"}
-    except Exception:
-        return None
+        return None, None
 
 
 def e2e_bench(args):
@@ -420,28 +503,115 @@ def stream_bench(args):
     print(json.dumps(line), flush=True)
 
 
+def sq_issue(kernel):
+    """Instruction-issue occupancy of `kernel` from the committed SQ PMC passes
+    (profiles/sq_issue.json, PROFILE-DERIVED): the binding resource of this integer
+    byte-shuffling path is instruction issue, not HBM."""
+    p = os.path.join(ROOT, "profiles", "sq_issue.json")
+    try:
+        d = json.load(open(p))[kernel]
+        return {"pipe": "valu", "busy": d["valu_pipe_busy"], "salu_busy": d["salu_busy"],
+                "source": "profiles/sq_issue.json (profile-derived)"}
+    except Exception:
+        return None
+
+
+def config2_leg(args, amd, torch, stream):
+    """BASELINE config 2 inside the default run: 262144 x 4 KiB random blocks, decompress
+    only, 1 MI355X.  The blocks are compressed by the reference algorithm -- the product's
+    host codec (ape_lz4_host.c, byte-identical to src/ape_lz4.c's compress_default on the
+    golden KATs) -- on the host, untimed, so the GPU decodes the reference's 4114-byte blocks,
+    not its own encoder's.  Timed: the decode kernel over all blocks, device-resident."""
+    n, nb = 4096, args.config2_blocks
+    L = amd.lib()
+    f = L.hst_compress_extstate
+    f.restype, f.argtypes = C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
+    src = torch.empty((nb, n), dtype=torch.uint8, device="cuda")
+    amd.synth_blocks(src, n, 0, 0)
+    host = src.cpu().numpy()
+    cap = amd.compressBound(n)
+    slot = (cap + 15) // 16 * 16
+    comp_h = np.zeros((nb, slot), dtype=np.uint8)
+    csz_h = np.zeros(nb, dtype=np.int32)
+    state = C.create_string_buffer(16416)
+    t0 = time.time()
+    base_in, base_out = host.ctypes.data, comp_h.ctypes.data
+    for b in range(nb):
+        csz_h[b] = f(state, base_in + b * n, base_out + b * slot, n, cap, 1)
+    log("[config2] %d blocks compressed by the host (reference) codec in %.1f s" % (
+        nb, time.time() - t0))
+    comp = torch.from_numpy(comp_h).cuda()
+    csz = torch.from_numpy(csz_h).cuda()
+    sizes = torch.full((nb,), n, dtype=torch.int32, device="cuda")
+    out = torch.empty((nb, n), dtype=torch.uint8, device="cuda")
+    res = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    for _ in range(max(1, args.warmup)):
+        amd.decompress_batch(comp, csz, out, res, dst_caps=sizes, stream=stream)
+    torch.cuda.synchronize()
+    steps = max(3, args.steps)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e in evs:
+        e[0].record(stream)
+        amd.decompress_batch(comp, csz, out, res, dst_caps=sizes, stream=stream)
+        e[1].record(stream)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+    ok = bool((res == n).all().item()) and bool(torch.equal(out, src))
+    cbytes = int(csz_h.astype(np.int64).sum())
+    alg = nb * n + cbytes
+    value = nb * n / wall / GIB
+    rd_bound = HBM_PEAK_GBPS * 1e9 / GIB * (nb * n) / cbytes   # read-only: c bytes per block
+    return {
+        "metric": "LZ4 GiB/s decompress-only, 256K x 4 KiB random blocks (BASELINE config 2)",
+        "value": round(value, 2), "unit": "GiB/s", "steps": steps,
+        "ms_per_step": round(wall * 1e3, 3),
+        "config": {"workload": "%d x 4 KiB random blocks (SURVEY App. C gen_rand), compressed "
+                               "by the reference algorithm on the host, decompress only" % nb},
+        "comp_bytes_min": int(csz_h.min()), "comp_bytes_max": int(csz_h.max()),
+        "reference_comp_bytes": 4114, "verified": ok,
+        "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "kernel": "lz4_decode_kernel", "bytes_per_launch": alg,
+                     "avg_launch_ms": round(ms, 3),
+                     "hbm_read_roofline_GiBps": round(rd_bound, 1),
+                     "hbm_read_frac": round(value / rd_bound, 4)},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--blocks", type=int, default=1 << 20, help="blocks per rank")
+    ap.add_argument("--blocks", type=int, default=1 << 20,
+                    help="total blocks of the job, split contiguously over the ranks "
+                         "(BASELINE config 4); per rank with --weak")
+    ap.add_argument("--weak", action="store_true", help="--blocks per rank (weak scaling)")
     ap.add_argument("--block-size", type=int, default=65536)
     ap.add_argument("--kind", choices=["comp", "rand"], default="comp")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-blocks", type=int, default=65536,
+                    help="CPU-baseline sample (65536 x 64 KiB = 4 GiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-config2", action="store_true")
+    ap.add_argument("--config2-blocks", type=int, default=1 << 18)
     ap.add_argument("--verify-sample", type=int, default=64)
     ap.add_argument("--e2e", action="store_true",
                     help="host->GPU->host socket-path rate instead of the device-resident line")
     ap.add_argument("--e2e-blocks", type=int, default=1 << 17)
     ap.add_argument("--e2e-chunk", type=int, default=1 << 14)
     ap.add_argument("--rand4k", action="store_true",
-                    help="BASELINE config 2: decompress-only over 4 KiB random blocks")
+                    help="BASELINE config 2 alone: decompress-only over 4 KiB random blocks")
     ap.add_argument("--rand4k-blocks", type=int, default=1 << 18)
     ap.add_argument("--stream", action="store_true",
                     help="chained-stream socket codec (withPrefix TX + usingDict RX)")
     ap.add_argument("--stream-blocks", type=int, default=1 << 17)
     ap.add_argument("--stream-chunk", type=int, default=8192)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
     if args.e2e:
         return e2e_bench(args)
@@ -453,7 +623,7 @@ def main():
     import torch
 
     import libapenetwork_amd as amd
-    from libapenetwork_amd.sharding import reduce_max, reduce_sum, shard
+    from libapenetwork_amd.sharding import gather, reduce_max, reduce_sum, shard, shard_strong
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -461,18 +631,26 @@ def main():
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
+        # no collective on the data path: the process group (gloo, host scalars) carries
+        # only the barrier, the max-over-ranks time and the per-rank numbers
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")
     rc = amd.gpu_init()
     if rc != 0:
         raise SystemExit("GPU codec unavailable: %s" % amd.gpu_last_error())
 
-    n, nb = args.block_size, args.blocks
+    n = args.block_size
+    if args.weak:
+        first, nb = shard(rank, world, args.blocks)
+        total_blocks = args.blocks * world
+    else:
+        first, nb = shard_strong(rank, world, args.blocks)
+        total_blocks = args.blocks
     kind = 1 if args.kind == "comp" else 0
     slot = (amd.compressBound(n) + 15) // 16 * 16
     stream = torch.cuda.current_stream()
-    log("[rank %d] allocating %.1f GiB (in %d x %d, slots %d)" % (
-        rank, nb * (2 * n + slot) / GIB, nb, n, slot))
+    log("[rank %d] blocks [%d, %d) of %d: allocating %.1f GiB (in %d x %d, slots %d)" % (
+        rank, first, first + nb, total_blocks, nb * (2 * n + slot) / GIB, nb, n, slot))
     src = torch.empty((nb, n), dtype=torch.uint8, device="cuda")
     comp = torch.empty((nb, slot), dtype=torch.uint8, device="cuda")
     out = torch.empty((nb, n), dtype=torch.uint8, device="cuda")
@@ -482,7 +660,6 @@ def main():
 
     t0 = time.time()
     chunk = 1 << 16
-    first, _ = shard(rank, world, nb)
     for b0 in range(0, nb, chunk):
         amd.synth_blocks(src[b0:b0 + chunk], n, first + b0, kind)
         torch.cuda.synchronize()
@@ -511,12 +688,13 @@ def main():
     for k in range(args.steps):
         step(evs[k])
     torch.cuda.synchronize()
+    mine = time.perf_counter() - t_start       # this rank's own time
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    elapsed = reduce_max(dist, elapsed, "cuda")
+    elapsed = reduce_max(dist, elapsed)
 
     # ---- correctness + ratio (outside the timed region) ----
     ok = bool((dres == n).all().item())
@@ -540,46 +718,82 @@ def main():
                 sample_ok &= (r == n and ob.raw[:n] == sb[j].tobytes())
         except OSError:
             sample_ok = None
-    comp_bytes, nok = reduce_sum(dist, [comp_bytes, int(ok)], "cuda")
+    per_rank = gather(dist, {"rank": rank, "blocks": nb, "first_block": first,
+                             "GiBps": round(nb * n / (mine / args.steps) / GIB, 2),
+                             "ms_per_step": round(mine / args.steps * 1e3, 3),
+                             "encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3)},
+                      world)
+    comp_total, nok = reduce_sum(dist, [comp_bytes, int(ok)])
     ok = nok == world
 
-    total_bytes = nb * n * world
+    total_bytes = total_blocks * n
     ms_step = elapsed / args.steps * 1e3
     value = total_bytes / (elapsed / args.steps) / GIB
-    ratio = total_bytes / max(comp_bytes, 1)
+    ratio = total_bytes / max(comp_total, 1)
 
-    # per-kernel roofline (this rank; algorithmic bytes = n + c per block per kernel)
-    alg = (nb * n + comp_bytes / world)
+    # ---- roofline (rank 0's kernels; algorithmic bytes) ----
+    # encode: read n + write c per block; decode: read c + write n per block.
+    alg = nb * n + comp_bytes
     enc_gbps = alg / (enc_ms * 1e-3) / 1e9
     dec_gbps = alg / (dec_ms * 1e-3) / 1e9
-    dom = "lz4_encode_kernel" if enc_ms >= dec_ms else "lz4_decode_kernel"
-    dom_gbps = enc_gbps if enc_ms >= dec_ms else dec_gbps
-    roof = {"bound": "hbm", "achieved": round(dom_gbps, 1), "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s", "frac": round(dom_gbps / HBM_PEAK_GBPS, 4),
-            "traffic": pmc_traffic(dom, nb), "kernel": dom,
-            "bytes_per_launch": int(alg),
-            "avg_launch_ms": round(enc_ms if enc_ms >= dec_ms else dec_ms, 3),
-            "issue": sq_issue(dom)}
+    enc_dom = enc_ms >= dec_ms
+    dom = "lz4_encode_kernel" if enc_dom else "lz4_decode_kernel"
+    traffic, tsrc = pmc_traffic(dom, nb)
+    step_s = ms_step * 1e-3
+    step_rw = 2 * (total_bytes + comp_total) / step_s / 1e9        # R+W of a round trip
+    step_rd = (total_bytes + comp_total) / step_s / 1e9            # reads only
+    # the north_star's "HBM-read roofline" in uncompressed GiB/s: a round trip reads
+    # n + c bytes per block, so HBM read peak x n / (n + c) bounds `value` (per GPU)
+    read_bound = HBM_PEAK_GBPS * 1e9 / GIB * total_bytes / (total_bytes + comp_total) * world
+    roof = {"bound": "hbm", "achieved": round(enc_gbps if enc_dom else dec_gbps, 1),
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round((enc_gbps if enc_dom else dec_gbps) / HBM_PEAK_GBPS, 4),
+            "traffic": traffic, "traffic_source": "profile-derived per block x blocks: %s" % tsrc,
+            "kernel": dom, "bytes_per_launch": int(alg),
+            "avg_launch_ms": round(enc_ms if enc_dom else dec_ms, 3),
+            "issue": sq_issue(dom),
+            "decoder": {"kernel": "lz4_decode_kernel", "achieved": round(dec_gbps, 1),
+                        "frac": round(dec_gbps / HBM_PEAK_GBPS, 4), "avg_launch_ms": round(dec_ms, 3)},
+            "encoder": {"kernel": "lz4_encode_kernel", "achieved": round(enc_gbps, 1),
+                        "frac": round(enc_gbps / HBM_PEAK_GBPS, 4), "avg_launch_ms": round(enc_ms, 3)},
+            "step": {"achieved_GBps": round(step_rw, 1),
+                     "frac": round(step_rw / (HBM_PEAK_GBPS * world), 4),
+                     "read_GBps": round(step_rd, 1),
+                     "read_frac": round(step_rd / (HBM_PEAK_GBPS * world), 4),
+                     "basis": "sum(n + c) x 2 (R+W) / step time, all ranks, vs 8 TB/s x GPUs"}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(n, kind, args.cpu_seconds)
+        cpu = cpu_baseline(n, kind, args.cpu_blocks)
+    c2 = None
+    if rank == 0 and world == 1 and not args.no_config2:
+        del src, comp, out
+        torch.cuda.empty_cache()
+        c2 = config2_leg(args, amd, torch, stream)
+        if not args.no_cpu_baseline:
+            c2["cpu_baseline"] = cpu_baseline(4096, 0, args.config2_blocks, mode=1)
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "higher_is_better": True, "scaling": "weak" if args.weak else "strong",
+            "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (SURVEY App. C gen_%s, seed = block id, generated on device)"
                     % args.kind,
-            "config": {"workload": "%d x %d KiB %s blocks per GPU, compress+decompress"
-                                   % (nb, n >> 10, "compressible" if kind else "random"),
-                       "blocks_per_gpu": nb, "block_bytes": n, "parallelism": "blocks%d" % world},
+            "config": {"workload": "%d x %d KiB %s blocks %s, compress+decompress" % (
+                           total_blocks, n >> 10, "compressible" if kind else "random",
+                           ("(%d per GPU)" % nb) if args.weak else "sharded over %d GPU" % world),
+                       "total_blocks": total_blocks, "blocks_per_gpu": nb, "block_bytes": n,
+                       "parallelism": "blocks%d" % world},
             "ratio": round(ratio, 4),
             "encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3),
             "encode_GBps": round(enc_gbps, 1), "decode_GBps": round(dec_gbps, 1),
+            "hbm_read_roofline": {"bound_GiBps": round(read_bound, 1),
+                                  "frac": round(value / read_bound, 4)},
+            "per_gpu": per_rank,
             "verified": bool(ok), "oracle_sample_ok": sample_ok,
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "config2": c2,
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -37,18 +37,31 @@ static void gpu_failed(int rt)
     }
 }
 
-static int gpu_compress(const char *src, char *dst, int n, int cap, int accel)
+/* One-shot compression routing.  The GPU encoder works on
+ * independent blocks of at most APE_LZ4_GPU_MAX_BLOCK (= the 64 KiB LZ4 window);
+ * a larger one-shot input -- which the reference compresses as one block with its
+ * byU32 table (ref src/ape_lz4.c:766-769, :530-755), up to LZ4_MAX_INPUT_SIZE --
+ * runs the host codec, whose output is byte-identical to the reference's.  This is
+ * a size rule, not a fallback: it applies with or without a GPU. */
+static int host_compress(void *state, const char *src, char *dst, int n, int cap, int accel)
+{
+    hst_stream st;
+    return hst_compress_extstate(state ? (hst_stream *)state : &st, src, dst, n, cap, accel);
+}
+
+static int gpu_compress_st(void *state, const char *src, char *dst, int n, int cap, int accel)
 {
     int rt = 0, r;
     if ((unsigned)n > (unsigned)LZ4_MAX_INPUT_SIZE) return 0; /* ref :558 */
+    if (n > APE_LZ4_GPU_MAX_BLOCK) return host_compress(state, src, dst, n, cap, accel);
     r = ape_lz4_gpu_compress_one(src, dst, n, cap, accel, &rt);
     if (rt) { gpu_failed(rt); return 0; }
-    if (r == APE_LZ4_GPU_ERANGE) {
-        fprintf(stderr, "libape_lz4_amd: block of %d bytes exceeds the GPU block limit (%d)\n",
-                n, APE_LZ4_GPU_MAX_BLOCK);
-        return 0;
-    }
-    return r;
+    return r == APE_LZ4_GPU_ERANGE ? 0 : r;
+}
+
+static int gpu_compress(const char *src, char *dst, int n, int cap, int accel)
+{
+    return gpu_compress_st(NULL, src, dst, n, cap, accel);
 }
 
 static int gpu_decompress(const char *src, char *dst, int csize, int cap, int partial, int target)
@@ -80,7 +93,7 @@ int APE_LZ4_compress_fast_extState(void *state, const char *source, char *dest, 
                                    int maxOutputSize, int acceleration)
 {
     APE_LZ4_resetStream((APE_LZ4_stream_t *)state); /* ref :762 */
-    return APE_LZ4_compress_fast(source, dest, inputSize, maxOutputSize, acceleration);
+    return gpu_compress_st(state, source, dest, inputSize, maxOutputSize, acceleration);
 }
 
 int APE_LZ4_compress_fast_force(const char *source, char *dest, int inputSize,

@@ -282,8 +282,9 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
         nd += __popcll(emit);
         if (emit) {
             const int last = 63 - __clzll((long long)emit);
-            // (FASTD: a final sequence's size is its literals; ob assumed a match)
-            op = lane_val(opl + ((FASTD && fin) ? lit : ob), last);
+            // a final sequence's size is its literals (ob assumed a match unless the
+            // input ended: a PARTIAL or FASTD stop by output size ends the block too)
+            op = lane_val(opl + (fin ? lit : ob), last);
         }
     }
     if (st == ST_MORE) P += (int)c;
@@ -500,9 +501,21 @@ lz4_decode_kernel(BlockArgs a) {
     Dec D;
     D.dst = (gu8 *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
     if (a.frame_off) {   // framed stream: [le32 size][block] (lz4_frame.hip)
-        gcu8 *f = (gcu8 *)(a.src_base + a.frame_off[b]);
-        D.csize = (int)((uint32_t)f[0] | ((uint32_t)f[1] << 8) | ((uint32_t)f[2] << 16) |
+        // The header is untrusted: it must fit the frame the offsets give (ref
+        // src/ape_socket.c:1382-1384 rejects a size above the data it has).  A frame
+        // shorter than its header, or a size < 0 or past the next frame, is malformed:
+        // -1, nothing read beyond the frame, nothing written.
+        const long long f0 = a.frame_off[b], avail = a.frame_off[b + 1] - f0 - 4;
+        int hdr = -1;
+        gcu8 *f = (gcu8 *)(a.src_base + f0);
+        if (avail >= 0)
+            hdr = (int)((uint32_t)f[0] | ((uint32_t)f[1] << 8) | ((uint32_t)f[2] << 16) |
                         ((uint32_t)f[3] << 24));
+        if (hdr < 0 || (long long)hdr > avail) {
+            if (lane == 0) a.result[b] = -1;
+            return;
+        }
+        D.csize = hdr;
         D.src = f + 4;
     } else {
         D.src = (gcu8 *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
@@ -546,6 +559,17 @@ lz4_decode_kernel(BlockArgs a) {
     D.s0 = stage_base(D.src, 0);
     stage_load(L, D.src, D.csize, D.s0, lane);
     wave_sync();
+    if (D.cap < 0) {
+        // oend < dest in the reference: the first sequence's literals already pass it,
+        // so its final-literals test fails (:1345-1366) -> -(ip)-1 after the token and
+        // its length bytes.  The scalar restatement computes exactly that (64-bit
+        // compares) and writes nothing; the window parser's unsigned cap would not.
+        int ip = 0, nd = 0;
+        uint32_t op0 = 0;
+        (void)parse_scalar<PARTIAL, FASTD>(L, D, ip, op0, nd, result);
+        if (lane == 0) a.result[b] = result;
+        return;
+    }
 
     // Output is copied in whole 256-byte steps: a batch copies up to the last step
     // boundary its sequences reach and carries the descriptors of the unfinished

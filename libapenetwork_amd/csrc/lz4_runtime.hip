@@ -61,7 +61,11 @@ int finish_launch(hipError_t e, const char *what) {
     return APE_LZ4_GPU_OK;
 }
 
-// ---- per-thread pinned staging for the host-buffer path ----
+// ---- pinned staging for the host-buffer path: a process-wide pool ----
+// A call borrows one context (stream + pinned + device staging) for its duration and
+// returns it, so concurrent callers never share staging, and a thread that exits holds
+// nothing (no thread-local HIP resources to leak).  Contexts whose staging grew past
+// kKeepBytes are freed on return instead of pooled.
 struct HostCtx {
     int dev = -1;
     hipStream_t stream = nullptr;
@@ -69,8 +73,6 @@ struct HostCtx {
     size_t hcap = 0;
     char *d = nullptr;  // device
     size_t dcap = 0;
-    // Trivially destructible on purpose: HIP may already be torn down when
-    // thread-exit destructors run; the staging is released on device change.
     void release() {
         if (h) (void)hipHostFree(h);
         if (d) (void)hipFree(d);
@@ -78,32 +80,61 @@ struct HostCtx {
         *this = HostCtx();
     }
 };
-thread_local HostCtx g_host;
+constexpr size_t kKeepBytes = 64u << 20;
+std::mutex g_pool_mu;
+std::vector<HostCtx *> g_pool;   // idle contexts (any device)
 
-int host_reserve(size_t bytes) {
+HostCtx *ctx_acquire() {
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (g_host.dev != dev) {
-        g_host.release();
-        g_host.dev = dev;
-        hipError_t e = hipStreamCreateWithFlags(&g_host.stream, hipStreamNonBlocking);
-        if (e != hipSuccess) { set_err("hipStreamCreate", e); return APE_LZ4_GPU_ENOMEM; }
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); i++) {
+            if (g_pool[i]->dev == dev) {
+                HostCtx *c = g_pool[i];
+                g_pool.erase(g_pool.begin() + (long)i);
+                return c;
+            }
+        }
     }
-    if (g_host.hcap < bytes) {
-        if (g_host.h) (void)hipHostFree(g_host.h);
-        g_host.h = nullptr;
-        size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
-        hipError_t e = hipHostMalloc((void **)&g_host.h, cap, hipHostMallocDefault);
-        if (e != hipSuccess) { g_host.hcap = 0; set_err("hipHostMalloc", e); return APE_LZ4_GPU_ENOMEM; }
-        g_host.hcap = cap;
+    HostCtx *c = new HostCtx();
+    c->dev = dev;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        set_err("hipStreamCreate", e);
+        delete c;
+        return nullptr;
     }
-    if (g_host.dcap < bytes) {
-        if (g_host.d) (void)hipFree(g_host.d);
-        g_host.d = nullptr;
+    return c;
+}
+
+void ctx_return(HostCtx *c) {
+    if (!c) return;
+    if (c->hcap > kKeepBytes || c->dcap > kKeepBytes) {
+        c->release();
+        delete c;
+        return;
+    }
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    g_pool.push_back(c);
+}
+
+int host_reserve(HostCtx &c, size_t bytes) {
+    if (c.hcap < bytes) {
+        if (c.h) (void)hipHostFree(c.h);
+        c.h = nullptr;
         size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
-        hipError_t e = hipMalloc((void **)&g_host.d, cap);
-        if (e != hipSuccess) { g_host.dcap = 0; set_err("hipMalloc", e); return APE_LZ4_GPU_ENOMEM; }
-        g_host.dcap = cap;
+        hipError_t e = hipHostMalloc((void **)&c.h, cap, hipHostMallocDefault);
+        if (e != hipSuccess) { c.hcap = 0; set_err("hipHostMalloc", e); return APE_LZ4_GPU_ENOMEM; }
+        c.hcap = cap;
+    }
+    if (c.dcap < bytes) {
+        if (c.d) (void)hipFree(c.d);
+        c.d = nullptr;
+        size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
+        hipError_t e = hipMalloc((void **)&c.d, cap);
+        if (e != hipSuccess) { c.dcap = 0; set_err("hipMalloc", e); return APE_LZ4_GPU_ENOMEM; }
+        c.dcap = cap;
     }
     return APE_LZ4_GPU_OK;
 }
@@ -113,6 +144,11 @@ inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
 // Staging layout (same offsets on host and device):
 //   [ptr arrays: src, dst][int arrays: in_size, cap, target, result][inputs][outputs]
 // mode: 0 = compress, 1 = decompress_safe, 2 = decompress_safe_partial
+int host_batch_run(HostCtx &ctx, int mode, int accel, const char *const *h_src, const int *h_in,
+                   char *const *h_dst, const int *h_cap, const int *h_target, int *h_res, int nb,
+                   const std::vector<size_t> &in_off, const std::vector<size_t> &out_off,
+                   const std::vector<size_t> &out_len, size_t total);
+
 int host_batch(int mode, int accel, const char *const *h_src, const int *h_in, char *const *h_dst,
                const int *h_cap, const int *h_target, int *h_res, int nb) {
     if (nb < 0 || (nb > 0 && (!h_src || !h_in || !h_dst || !h_cap || !h_res))) {
@@ -138,15 +174,31 @@ int host_batch(int mode, int accel, const char *const *h_src, const int *h_in, c
             size_t bound = (size_t)n + n / 255 + 16;
             lim = h_cap[i] <= 0 ? 0 : ((size_t)h_cap[i] < bound ? (size_t)h_cap[i] : bound);
         } else {
-            lim = h_cap[i] <= 0 ? 0 : (size_t)h_cap[i];  // the decoder has no block limit
+            // the decoder writes only decoded bytes, and LZ4 expands at most 255x (a
+            // 255 length byte per 255 output bytes): a huge cap needs no huge staging
+            const size_t cs = h_in[i] > 0 ? (size_t)h_in[i] : 0;
+            const size_t most = 255 * cs + 64;
+            lim = h_cap[i] <= 0 ? 0 : ((size_t)h_cap[i] < most ? (size_t)h_cap[i] : most);
         }
         out_len[i] = lim;
         pos += up16(lim ? lim : 1);
     }
     const size_t total = pos;
-    rc = host_reserve(total);
-    if (rc) return rc;
-    char *H = g_host.h, *D = g_host.d;
+    HostCtx *ctx = ctx_acquire();
+    if (!ctx) return APE_LZ4_GPU_ENOMEM;
+    rc = host_reserve(*ctx, total);
+    if (rc) { ctx_return(ctx); return rc; }
+    rc = host_batch_run(*ctx, mode, accel, h_src, h_in, h_dst, h_cap, h_target, h_res, nb,
+                        in_off, out_off, out_len, total);
+    ctx_return(ctx);
+    return rc;
+}
+
+int host_batch_run(HostCtx &ctx, int mode, int accel, const char *const *h_src, const int *h_in,
+                   char *const *h_dst, const int *h_cap, const int *h_target, int *h_res, int nb,
+                   const std::vector<size_t> &in_off, const std::vector<size_t> &out_off,
+                   const std::vector<size_t> &out_len, size_t total) {
+    char *H = ctx.h, *D = ctx.d;
     const char **hp_src = (const char **)H;
     char **hp_dst = (char **)(H + (size_t)nb * sizeof(void *));
     int *hi = (int *)(H + up16((size_t)nb * 2 * sizeof(void *)));
@@ -161,7 +213,7 @@ int host_batch(int mode, int accel, const char *const *h_src, const int *h_in, c
         if (h_in[i] > 0) memcpy(H + in_off[i], h_src[i], (size_t)h_in[i]);
         else H[in_off[i]] = h_src[i] ? h_src[i][0] : 0;
     }
-    hipStream_t s = g_host.stream;
+    hipStream_t s = ctx.stream;
     hipError_t e = hipMemcpyAsync(D, H, out_off[0], hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return finish_launch(e, "hipMemcpyAsync H2D");
     BlockArgs a{};

@@ -1,13 +1,24 @@
-"""Block sharding across ranks for the batched codec.
+"""Block sharding across ranks for the batched codec (BASELINE config 4).
 
-The path shards naturally: blocks are independent, so rank r of W takes the
-contiguous block range [r*N, (r+1)*N) of a global batch (weak scaling: N blocks
-per rank), with its own inputs, output slots and size/status arrays.  There is no
-collective on the data path; the only cross-rank operations are the benchmark's
-barrier, the max-over-ranks step time and the sum of per-rank byte counts, all on
-scalars.  Works with any torch.distributed backend (RCCL/"nccl" on the GPUs, "gloo"
-in the CPU tests).
+The path shards naturally: blocks are independent.  BASELINE config 4 is "1M x 64 KiB
+blocks sharded across 8 MI355X": a fixed total batch of N blocks split contiguously,
+rank r of W taking blocks [r*N//W, (r+1)*N//W) (strong scaling; 131072 blocks per GPU
+at N = 1M, W = 8), each rank with its own inputs, output slots and size/status arrays.
+Weak scaling (N blocks per rank) stays available as an opt-in.
+
+There is no collective on the data path and no RCCL at all: the only cross-rank
+operations are the benchmark's barrier, the max-over-ranks step time and the gather of
+per-rank scalars, all on host scalars over a gloo (CPU) process group.
 """
+
+
+def shard_strong(rank, world, total_blocks):
+    """(first_block, nblocks) of `rank`: the contiguous split of a fixed batch."""
+    if world < 1 or not 0 <= rank < world or total_blocks < 0:
+        raise ValueError("bad shard request: rank %r of %r, %r blocks" % (rank, world,
+                                                                          total_blocks))
+    first = rank * total_blocks // world
+    return first, (rank + 1) * total_blocks // world - first
 
 
 def shard(rank, world, blocks_per_rank):
@@ -18,7 +29,7 @@ def shard(rank, world, blocks_per_rank):
     return rank * blocks_per_rank, blocks_per_rank
 
 
-def reduce_max(dist, value, device):
+def reduce_max(dist, value, device="cpu"):
     """Max of a float over ranks (the benchmark's step time); identity without dist."""
     if dist is None:
         return float(value)
@@ -28,7 +39,7 @@ def reduce_max(dist, value, device):
     return float(t.item())
 
 
-def reduce_sum(dist, values, device):
+def reduce_sum(dist, values, device="cpu"):
     """Elementwise sum of a list of ints over ranks; identity without dist."""
     if dist is None:
         return [int(v) for v in values]
@@ -36,3 +47,12 @@ def reduce_sum(dist, values, device):
     t = torch.tensor([int(v) for v in values], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [int(v) for v in t.tolist()]
+
+
+def gather(dist, obj, world):
+    """Every rank's `obj` (list indexed by rank); [obj] without dist."""
+    if dist is None:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out

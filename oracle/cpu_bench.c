@@ -235,3 +235,122 @@ int cpu_stream_run(const char *lib, const char *prefix, int nthreads, int nblock
     dlclose(h);
     return 0;
 }
+
+/*
+ * Handle-based form (bench.py's thread sweep): the sample is
+ * generated once (in parallel, untimed, pre-faulted), compressed once untimed so
+ * decode-only timings have input, then timed at any number of thread counts.
+ *   h = cpu_bench_prepare(lib, prefix, nblocks, n, kind, gen_threads)
+ *   cpu_bench_time(h, nthreads, reps, mode, out)   mode 0 = compress + decompress,
+ *                                                  mode 1 = decompress only
+ *   cpu_bench_free(h)
+ * out[] as cpu_bench_run.  Every timed decompress is checked against the input.
+ */
+typedef struct {
+    void *dl;
+    comp_fn comp;
+    dec_fn dec;
+    uint8_t *in, *cmp, *out;
+    int *csz;
+    int n, cap, nblocks;
+} bench_t;
+
+typedef struct {
+    uint8_t *out;
+    int n, kind;
+    long long first;
+    int count;
+} gen_t;
+
+static void *gen_worker(void *arg)
+{
+    gen_t *g = (gen_t *)arg;
+    if (g->count > 0) synth_blocks(g->out, g->n, g->n, g->first, g->count, g->kind);
+    return NULL;
+}
+
+void *cpu_bench_prepare(const char *lib, const char *prefix, int nblocks, int n, int kind,
+                        int gen_threads)
+{
+    char name[128];
+    bench_t *b = calloc(1, sizeof *b);
+    if (!b || nblocks < 1 || n < 1) { free(b); return NULL; }
+    b->dl = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+    if (!b->dl) { fprintf(stderr, "cpu_bench: %s\n", dlerror()); free(b); return NULL; }
+    snprintf(name, sizeof name, "%scompress_default", prefix);
+    b->comp = (comp_fn)dlsym(b->dl, name);
+    snprintf(name, sizeof name, "%sdecompress_safe", prefix);
+    b->dec = (dec_fn)dlsym(b->dl, name);
+    b->n = n;
+    b->cap = n + n / 255 + 16;
+    b->nblocks = nblocks;
+    b->in = malloc((size_t)nblocks * n);
+    b->cmp = malloc((size_t)nblocks * b->cap);
+    b->out = malloc((size_t)nblocks * n);
+    b->csz = calloc((size_t)nblocks, sizeof(int));
+    if (!b->comp || !b->dec || !b->in || !b->cmp || !b->out || !b->csz) {
+        free(b->in); free(b->cmp); free(b->out); free(b->csz);
+        dlclose(b->dl);
+        free(b);
+        return NULL;
+    }
+    if (gen_threads < 1) gen_threads = 1;
+    if (gen_threads > 256) gen_threads = 256;
+    pthread_t th[256];
+    gen_t g[256];
+    for (int i = 0; i < gen_threads; i++) {
+        long long b0 = (long long)nblocks * i / gen_threads, b1 = (long long)nblocks * (i + 1) / gen_threads;
+        g[i] = (gen_t){b->in + b0 * n, n, kind, b0, (int)(b1 - b0)};
+        pthread_create(&th[i], NULL, gen_worker, &g[i]);
+    }
+    for (int i = 0; i < gen_threads; i++) pthread_join(th[i], NULL);
+    memset(b->out, 0, (size_t)nblocks * n); /* pre-fault */
+    /* one untimed compress (also pre-faults cmp) so decode-only runs have input */
+    task_t tasks[256];
+    for (int i = 0; i < gen_threads; i++)
+        tasks[i] = (task_t){b->comp, b->dec, b->in, b->cmp, b->out, b->csz, n, b->cap,
+                            (int)((long long)nblocks * i / gen_threads),
+                            (int)((long long)nblocks * (i + 1) / gen_threads), 0, 0};
+    run_phase(tasks, gen_threads, 0);
+    return b;
+}
+
+int cpu_bench_time(void *h, int nthreads, int reps, int mode, double *out)
+{
+    bench_t *b = (bench_t *)h;
+    if (!b || nthreads < 1 || nthreads > 256 || reps < 1) return -1;
+    task_t tasks[256];
+    for (int i = 0; i < nthreads; i++)
+        tasks[i] = (task_t){b->comp, b->dec, b->in, b->cmp, b->out, b->csz, b->n, b->cap,
+                            (int)((long long)b->nblocks * i / nthreads),
+                            (int)((long long)b->nblocks * (i + 1) / nthreads), 0, 0};
+    if (mode == 0) run_phase(tasks, nthreads, 0); /* warm-up */
+    run_phase(tasks, nthreads, 1);
+    for (int i = 0; i < nthreads; i++) tasks[i].bad = 0;
+    double tc = 0, td = 0;
+    for (int r = 0; r < reps; r++) {
+        if (mode == 0) tc += run_phase(tasks, nthreads, 0);
+        td += run_phase(tasks, nthreads, 1);
+    }
+    long long tot = 0;
+    int bad = 0;
+    for (int k = 0; k < b->nblocks; k++) tot += b->csz[k];
+    for (int i = 0; i < nthreads; i++) bad += tasks[i].bad;
+    if (memcmp(b->in, b->out, (size_t)b->nblocks * b->n) != 0) bad++;
+    memset(b->out, 0, (size_t)b->nblocks * b->n);
+    out[0] = tc;
+    out[1] = td;
+    out[2] = (double)tot;
+    out[3] = bad;
+    out[4] = (double)b->nblocks * b->n;
+    return 0;
+}
+
+void cpu_bench_free(void *h)
+{
+    bench_t *b = (bench_t *)h;
+    if (!b) return;
+    free(b->in); free(b->cmp); free(b->out); free(b->csz);
+    dlclose(b->dl);
+    free(b);
+}

@@ -46,6 +46,15 @@ def product():
     return amd
 
 
+@pytest.fixture(autouse=True)
+def _dst_canaries(request):
+    """After every GPU test: nothing was written outside any alloc_out() slot."""
+    yield
+    if request.node.get_closest_marker("gpu") is not None:
+        import gpuutil
+        gpuutil.check_canaries()
+
+
 @pytest.fixture(scope="session")
 def cuda():
     import torch

@@ -216,6 +216,21 @@ def main():
                              "frames_b64": [base64.b64encode(f).decode() for f in frames],
                              "dec_rets": rets, "plain_sha256": I.sha(plain),
                              "plain_ok": plain == b"".join(msgs)})
+    # 5. benchmark-size decode KATs (pin 64 KiB decode parity on reference
+    #    output, not only on the restatement): BASELINE config 3 blocks (App. C gen_comp,
+    #    65536 B) and config 2 blocks (gen_rand, 4096 B), compressed by the reference
+    brng = random.Random(20261016)
+    for bid in (0, 1, 777, 65535, 524287, 1048575):
+        src = I.synth_comp(65536, bid)
+        _, comp = compress(src, F("compressBound")(65536))
+        for cap in (65536, 65535):
+            fx["decode"].append(dec_case("bench_comp64k_%d_cap%d" % (bid, cap), comp, cap, brng))
+    for bid in (0, 1, 4242, 262143):
+        src = I.synth_rand(4096, bid)
+        _, comp = compress(src, F("compressBound")(4096))
+        assert len(comp) == 4114
+        for cap in (4096, 4095):
+            fx["decode"].append(dec_case("bench_rand4k_%d_cap%d" % (bid, cap), comp, cap, brng))
     out = os.path.join(HERE, "lz4_golden.json")
     with open(out, "w") as f:
         json.dump(fx, f, separators=(",", ":"))

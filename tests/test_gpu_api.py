@@ -89,3 +89,73 @@ def test_device_generator_matches_spec(cuda, product, oracle):
         h = t.cpu().numpy()
         for b in range(5):
             assert h[b, :n].tobytes() == fn(n, 1000 + b)
+
+
+def test_concurrent_one_shot_callers(cuda, product, oracle):
+    """SURVEY 8(b) threading: the shim is thread-safe per call.  8 threads issue one-shot
+    compress_default / decompress_safe / decompress_safe_partial calls at once (ctypes drops
+    the GIL around each call); every result must equal the single-threaded one."""
+    import threading
+    L = product.lib()
+    srcs = [I.make(c, n, seed=n + k) for k, (c, n) in enumerate(
+        [("comp", 65536), ("text", 30000), ("rand", 4096), ("zeros", 65536), ("comp", 1000),
+         ("period7", 20000), ("comp", 65537), ("text", 200000)])]
+    expect = []
+    for s in srcs:
+        r, comp = product.compress_default(s)
+        assert r > 0 and orc_decompress(oracle, comp, len(s)) == (len(s), s)
+        expect.append(comp)
+    errors = []
+
+    def worker(t):
+        try:
+            for it in range(12):
+                i = (t + it) % len(srcs)
+                s = srcs[i]
+                o = C.create_string_buffer(product.compressBound(len(s)) + 64)
+                r = L.APE_LZ4_compress_default(buf(s), o, len(s), product.compressBound(len(s)))
+                if o.raw[:r] != expect[i]:
+                    errors.append(("compress", t, i, r))
+                d = C.create_string_buffer(len(s) + 64)
+                r2 = L.APE_LZ4_decompress_safe(buf(expect[i]), d, len(expect[i]), len(s))
+                if r2 != len(s) or d.raw[:len(s)] != s:
+                    errors.append(("decompress", t, i, r2))
+                p = C.create_string_buffer(len(s) + 64)
+                r3 = L.APE_LZ4_decompress_safe_partial(buf(expect[i]), p, len(expect[i]),
+                                                       len(s) // 2, len(s))
+                if r3 < len(s) // 2 or p.raw[:len(s) // 2] != s[:len(s) // 2]:
+                    errors.append(("partial", t, i, r3))
+        except Exception as e:   # pragma: no cover
+            errors.append(("exception", t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:5]
+
+
+def test_one_shot_latency_recorded(cuda, product):
+    """One-call latency of the GPU one-shot path next to the host codec, for the routing
+    note in DESIGN.md: printed, and sanity-bounded only."""
+    import time
+    L = product.lib()
+    for n in (4096, 65536):
+        s = I.make("comp", n, seed=5)
+        o = C.create_string_buffer(product.compressBound(n) + 64)
+        b = buf(s)
+        for _ in range(3):
+            L.APE_LZ4_compress_default(b, o, n, product.compressBound(n))
+        t0 = time.perf_counter()
+        for _ in range(20):
+            r = L.APE_LZ4_compress_default(b, o, n, product.compressBound(n))
+        dt = (time.perf_counter() - t0) / 20
+        d = C.create_string_buffer(n + 64)
+        cb = buf(o.raw[:r])
+        t0 = time.perf_counter()
+        for _ in range(20):
+            L.APE_LZ4_decompress_safe(cb, d, r, n)
+        dd = (time.perf_counter() - t0) / 20
+        print("one-shot n=%d: compress %.1f us, decompress %.1f us" % (n, dt * 1e6, dd * 1e6))
+        assert dt < 0.5 and dd < 0.5

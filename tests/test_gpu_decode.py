@@ -81,7 +81,10 @@ def test_fuzz_malformed_vs_oracle(cuda, product, oracle):
         if rng.random() < 0.2:
             c = c[:rng.randrange(len(c) + 1)]
         comps.append(bytes(c))
-        caps.append(max(0, rng.choice([n, n - 1, n + 40, rng.randrange(n + 1), 65536])))
+        cap = max(0, rng.choice([n, n - 1, n + 40, rng.randrange(n + 1), 65536]))
+        if rng.random() < 0.05:   # negative caps: oend < dest in the reference
+            cap = rng.choice([-1, -2, -13, -rng.randrange(1, 1 << 20)])
+        caps.append(cap)
         tg.append(rng.randrange(-5, n + 40))
     for targets in (None, tg):
         rs, outs = run_decode(cuda, product, comps, caps, targets=targets)
@@ -232,3 +235,75 @@ def test_decompress_fast_garbage_stays_in_bounds(cuda, product, oracle):
     cuda.cuda.synchronize()
     for b, r in zip(blobs, res.cpu().tolist()):
         assert r <= len(b)
+
+
+def test_negative_capacity(cuda, product, oracle):
+    """decompress_safe / _partial / _fast with a negative capacity: the
+    reference fails the first sequence (oend < dest) and writes nothing; same code here,
+    and the canary check proves nothing was written."""
+    import ctypes as C
+    from lz4util import buf
+    srcs = [I.make(c, n, seed=n) for c in ("comp", "text", "rand", "zeros") for n in (13, 100, 4096, 65536)]
+    comps = [orc_compress(oracle, s)[1] for s in srcs]
+    comps += [b"\xf0" + b"\xff" * 40 + b"\x00", b"\x00", b"\x1f\x41\x01\x00"]
+    caps = [-1, -5, -65536, -(1 << 30)]
+    cases = [(c, cap) for c in comps for cap in caps]
+    blobs = [c for c, _ in cases]
+    cps = [cap for _, cap in cases]
+    rs, _ = run_decode(cuda, product, blobs, cps)
+    assert rs == [orc_decompress(oracle, c, cap)[0] for c, cap in cases]
+    rs, _ = run_decode(cuda, product, blobs, cps, targets=[abs(cap) for cap in cps])
+    assert rs == [orc_decompress(oracle, c, cap, abs(cap))[0] for c, cap in cases]
+    ins, iptr, _ = pack(cuda, blobs)
+    dst, dptr, doffs = alloc_out(cuda, [0] * len(cases))
+    res = ints(cuda, [0] * len(cases))
+    product.decompress_fast_ptr_batch(iptr, ints(cuda, [len(b) for b in blobs]), dptr,
+                                      ints(cuda, cps), res)
+    cuda.cuda.synchronize()
+    exp = [oracle.orc_decompress_fast(buf(c), C.create_string_buffer(64), cap) for c, cap in cases]
+    assert res.cpu().tolist() == exp
+
+
+def _ref_lib():
+    import ctypes as C
+    import os
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                     "oracle", "_ref", "libape_lz4_ref.so")
+    if not os.path.exists(p):
+        pytest.skip("oracle/_ref (the reference built from its own source) not present")
+    return C.CDLL(p)
+
+
+@pytest.mark.parametrize("cfg", ["config3_comp64k", "config2_rand4k"])
+def test_benchmark_blocks_vs_reference_itself(cuda, product, cfg):
+    """decode reference-compressed benchmark blocks (BASELINE config 3:
+    App. C gen_comp 64 KiB; config 2: gen_rand 4 KiB) on the GPU and compare the return
+    value and bytes with the reference decoder itself (oracle/_ref, compiled from
+    src/ape_lz4.c), at the exact cap and one byte short."""
+    import ctypes as C
+    from lz4util import buf
+    ref = _ref_lib()
+    torch = cuda
+    n, kind, nb, first = ((65536, 1, 192, 1048576 - 96) if cfg == "config3_comp64k"
+                          else (4096, 0, 512, 262144 - 256))
+    t = torch.empty((nb, n), dtype=torch.uint8, device="cuda")
+    product.synth_blocks(t, n, first, kind)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy()
+    bound = product.compressBound(n)
+    comps = []
+    for b in range(nb):
+        o = C.create_string_buffer(bound + 64)
+        r = ref.APE_LZ4_compress_default(buf(host[b].tobytes()), o, n, bound)
+        assert r > 0
+        comps.append(o.raw[:r])
+    if kind == 0:
+        assert {len(c) for c in comps} == {4114}
+    for cap in (n, n - 1):
+        rs, outs = run_decode(cuda, product, comps, [cap] * nb)
+        for b, (c, r, out) in enumerate(zip(comps, rs, outs)):
+            o = C.create_string_buffer(cap + 64)
+            er = ref.APE_LZ4_decompress_safe(buf(c), o, len(c), cap)
+            assert r == er, (b, cap, r, er)
+            if er > 0:
+                assert out == o.raw[:er] == host[b].tobytes()[:er], (b, cap)

@@ -109,3 +109,44 @@ def test_frames_malformed_block_reports_like_decompress_safe(cuda, product):
     r = res.cpu().tolist()
     assert r == res2.cpu().tolist()
     assert r[0] == 4096 and r[2] == 4096 and r[1] < 0
+
+
+def test_frames_corrupt_header_is_rejected(cuda, product):
+    """a frame header claiming more bytes than its frame holds (or a negative
+    size) is rejected with -1 before anything is read past the frame or written; the
+    neighbouring frames decode normally (ref src/ape_socket.c:1382-1384 rejects a size
+    above the data it has)."""
+    torch = cuda
+    amd = product
+    nb, n = 6, 4096
+    srcs = [I.make("comp", n, seed=40 + s) for s in range(nb)]
+    host = np.stack([np.frombuffer(s, dtype=np.uint8) for s in srcs])
+    src = torch.from_numpy(host).cuda()
+    sizes = torch.full((nb,), n, dtype=torch.int32, device="cuda")
+    slot = (amd.compressBound(n) + 15) // 16 * 16
+    comp = torch.zeros((nb, slot), dtype=torch.uint8, device="cuda")
+    csz = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    amd.compress_batch(src, sizes, comp, csz)
+    off = torch.zeros(nb + 1, dtype=torch.int64, device="cuda")
+    amd.frame_offsets(csz, off)
+    frames = torch.zeros(int(off[-1].item()) + 64, dtype=torch.uint8, device="cuda")
+    amd.frame_pack(comp, csz, off, frames)
+    torch.cuda.synchronize()
+    o = off.cpu().tolist()
+    fh = frames.cpu().numpy()
+    big = (int(csz[1].item()) + 1).to_bytes(4, "little")        # one byte past its frame
+    fh[o[1]:o[1] + 4] = np.frombuffer(big, dtype=np.uint8)
+    fh[o[3]:o[3] + 4] = np.frombuffer((0x80000001).to_bytes(4, "little"), dtype=np.uint8)
+    fh[o[4]:o[4] + 4] = np.frombuffer((0x7FFFFFF0).to_bytes(4, "little"), dtype=np.uint8)
+    frames = torch.from_numpy(fh).cuda()
+    out = torch.full((nb, n), 0xCB, dtype=torch.uint8, device="cuda")
+    res = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    amd.decompress_frames(frames, off, out, res, dst_caps=sizes)
+    torch.cuda.synchronize()
+    r = res.cpu().tolist()
+    assert r == [n, -1, n, -1, -1, n], r
+    oh = out.cpu().numpy()
+    for i in (1, 3, 4):
+        assert (oh[i] == 0xCB).all(), i
+    for i in (0, 2, 5):
+        assert oh[i].tobytes() == srcs[i]

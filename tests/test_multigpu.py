@@ -1,9 +1,12 @@
-"""The N>1 path on CPU: world_size-2 gloo ranks run the benchmark's sharding and
-reductions (libapenetwork_amd.sharding) over the same synthetic blocks, each rank
-compressing/decompressing its own shard with the oracle (the GPU kernels are not
-available here).  Checks: shards are disjoint and cover the batch, each rank's data
-is the global data's slice, per-rank results reduce to the single-process totals,
-and the max-over-ranks time is the slowest rank's.
+"""The N>1 path on CPU (BASELINE config 4): world_size-2 gloo ranks run the
+benchmark's strong sharding and host-scalar reductions (libapenetwork_amd.sharding) over
+one fixed batch of synthetic blocks.  Each rank compresses and decompresses its own shard
+through the PRODUCT library's host codec (ape_lz4_host.c: the reference's compress_default
+/ decompress_safe restated bit-exactly -- the GPU kernels are not available here), and
+the oracle checks the bytes.  Checks: shards are disjoint, contiguous and cover the batch;
+each rank's blocks are the global batch's slice; per-rank compressed sizes reduce to the
+single-process totals; the max-over-ranks time is the slowest rank's; no collective other
+than the gloo scalar ones is used.
 """
 import ctypes as C
 import os
@@ -14,7 +17,7 @@ import pytest
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-N, PER_RANK, WORLD = 4096, 6, 2
+N, TOTAL, WORLD = 4096, 13, 2     # 13 blocks: an uneven split (6 + 7)
 
 
 def _free_port():
@@ -25,48 +28,91 @@ def _free_port():
     return port
 
 
+def _product_host_codec():
+    import libapenetwork_amd as amd
+    L = amd.lib()
+    L.hst_compress_extstate.restype = C.c_int
+    L.hst_compress_extstate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                        C.c_int]
+    L.hst_decompress_usingDict.restype = C.c_int
+    L.hst_decompress_usingDict.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                           C.c_void_p, C.c_int]
+    return L
+
+
 def _shard_stats(orc, first, count):
-    """(compressed bytes, xor checksum of the blocks) of blocks [first, first+count)."""
-    buf = C.create_string_buffer(N * count)
-    orc.synth_blocks(buf, N, C.c_longlong(N), C.c_longlong(first), count, 1)
+    """Product host codec over blocks [first, first+count): (compressed bytes, crc list)."""
+    L = _product_host_codec()
+    buf = C.create_string_buffer(N * max(count, 1))
+    if count:
+        orc.synth_blocks(buf, N, C.c_longlong(N), C.c_longlong(first), count, 1)
     cap = orc.orc_compressBound(N)
     out, dec = C.create_string_buffer(cap + 64), C.create_string_buffer(N + 64)
-    total, ck = 0, 0
+    state = C.create_string_buffer(16416)
+    ref = C.create_string_buffer(cap + 64)
+    total, cks = 0, []
     for b in range(count):
         blk = buf.raw[b * N:(b + 1) * N]
-        r = orc.orc_compress_default(C.create_string_buffer(blk, N + 16), out, N, cap)
-        assert r > 0
-        assert orc.orc_decompress_safe(out, dec, r, N) == N and dec.raw[:N] == blk
+        src = C.create_string_buffer(blk, N + 16)
+        r = L.hst_compress_extstate(state, src, out, N, cap, 1)
+        # the product's host codec is the reference's compress_default (oracle-checked)
+        er = orc.orc_compress_default(src, ref, N, cap)
+        assert r == er and out.raw[:r] == ref.raw[:r]
+        assert L.hst_decompress_usingDict(out, dec, r, N, 1, None, 0) == N and dec.raw[:N] == blk
         total += r
-        ck ^= zlib.crc32(blk)
-    return total, ck
+        cks.append(zlib.crc32(blk))
+    return total, cks
 
 
 def _worker(rank, port, q):
     import torch.distributed as dist
-    from libapenetwork_amd.sharding import reduce_max, reduce_sum, shard
+    from libapenetwork_amd.sharding import gather, reduce_max, reduce_sum, shard_strong
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     try:
         orc = C.CDLL(os.path.join(ROOT, "oracle", "liblz4_oracle.so"))
-        first, count = shard(rank, WORLD, PER_RANK)
-        comp, ck = _shard_stats(orc, first, count)
-        elapsed = reduce_max(dist, 1.0 + rank, "cpu")   # rank 1 is the slow one
-        tot_comp, tot_ok = reduce_sum(dist, [comp, 1], "cpu")
-        ranges = [None] * WORLD
-        dist.all_gather_object(ranges, (first, count, ck))
+        first, count = shard_strong(rank, WORLD, TOTAL)
+        comp, cks = _shard_stats(orc, first, count)
+        dist.barrier()
+        elapsed = reduce_max(dist, 1.0 + rank)   # rank 1 is the slow one
+        tot_comp, tot_ok = reduce_sum(dist, [comp, 1])
+        ranges = gather(dist, (first, count, cks), WORLD)
         q.put((rank, elapsed, tot_comp, tot_ok, ranges))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharding_unit():
-    from libapenetwork_amd.sharding import reduce_max, reduce_sum, shard
+def test_strong_shard_mapping():
+    """Config 4: 1,048,576 blocks over N = 1, 2, 4, 8 GPUs -> contiguous equal shards
+    (131072 per GPU at N = 8); uneven totals differ by at most one block per rank."""
+    from libapenetwork_amd.sharding import shard, shard_strong
+    for world in (1, 2, 4, 8):
+        parts = [shard_strong(r, world, 1 << 20) for r in range(world)]
+        assert all(c == (1 << 20) // world for _, c in parts)
+        assert [f for f, _ in parts] == [r * ((1 << 20) // world) for r in range(world)]
+    assert shard_strong(7, 8, 1 << 20) == (7 * 131072, 131072)
+    for total in (0, 1, 7, 13, 1000003):
+        for world in (1, 2, 3, 8):
+            parts = [shard_strong(r, world, total) for r in range(world)]
+            assert sum(c for _, c in parts) == total
+            assert all(parts[r][0] + parts[r][1] == parts[r + 1][0] for r in range(world - 1))
+            assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
     assert [shard(r, 4, 10) for r in range(4)] == [(0, 10), (10, 10), (20, 10), (30, 10)]
     with pytest.raises(ValueError):
-        shard(4, 4, 10)
-    assert reduce_max(None, 2.5, "cpu") == 2.5
-    assert reduce_sum(None, [3, 4], "cpu") == [3, 4]
+        shard_strong(8, 8, 10)
+
+
+def test_reductions_without_dist():
+    from libapenetwork_amd.sharding import gather, reduce_max, reduce_sum
+    assert reduce_max(None, 2.5) == 2.5
+    assert reduce_sum(None, [3, 4]) == [3, 4]
+    assert gather(None, {"a": 1}, 1) == [{"a": 1}]
+
+
+def test_bench_uses_no_rccl():
+    """bench.py's process group is gloo (host scalars only): no RCCL on the path."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'init_process_group("gloo")' in src and '"nccl"' not in src
 
 
 def test_two_rank_gloo(oracle):
@@ -80,12 +126,9 @@ def test_two_rank_gloo(oracle):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # single-process reference over the whole batch
-    total, _ = _shard_stats(oracle, 0, WORLD * PER_RANK)
+    total, all_cks = _shard_stats(oracle, 0, TOTAL)   # single process over the whole batch
     for rank, elapsed, tot_comp, tot_ok, ranges in res:
         assert elapsed == 2.0                      # max over ranks
         assert tot_comp == total and tot_ok == WORLD
-        covered = sorted((f, f + c) for f, c, _ in ranges)
-        assert covered == [(0, PER_RANK), (PER_RANK, 2 * PER_RANK)]   # disjoint, covering
-        for f, c, ck in ranges:
-            assert ck == _shard_stats(oracle, f, c)[1]
+        assert [(f, c) for f, c, _ in ranges] == [(0, 6), (6, 7)]   # disjoint, covering
+        assert [ck for _, _, cks in ranges for ck in cks] == all_cks

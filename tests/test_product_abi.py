@@ -189,3 +189,40 @@ def test_no_gpu_fails_loudly(product):
     assert r == 0
     r, _ = product.decompress_safe(b"\x50hello", 5)
     assert r < 0
+
+
+def test_one_shot_compress_above_gpu_block(product, golden, oracle):
+    """compress_default / compress_fast / _extState on inputs above the GPU block limit
+    (65536 < n <= LZ4_MAX_INPUT_SIZE) run the host codec and return the reference's exact
+    block (ref src/ape_lz4.c:766-769 byU32 path), GPU or not."""
+    from lz4util import blob_matches
+    import base64
+    L = product.lib()
+    kats = [e for e in golden["encode"] if e["n"] > 65536]
+    assert {e["n"] for e in kats} == {65546, 65547}
+    for e in kats:
+        src = I.make(e["content"], e["n"])
+        assert sha(src) == e["in_sha256"]
+        out = C.create_string_buffer(e["bound"] + 64)
+        r = L.APE_LZ4_compress_default(buf(src), out, e["n"], e["bound"])
+        assert r == e["clen"] and blob_matches(e["comp"], out.raw[:r]), (e["content"], e["n"])
+        for lim in e["limited"]:
+            o2 = C.create_string_buffer(max(lim["cap"], 1) + 64)
+            assert L.APE_LZ4_compress_default(buf(src), o2, e["n"], lim["cap"]) == lim["ret"]
+        for ac in e["accel"]:
+            o3 = C.create_string_buffer(e["bound"] + 64)
+            r3 = L.APE_LZ4_compress_fast(buf(src), o3, e["n"], e["bound"], ac["accel"])
+            assert r3 == ac["ret"] and sha(o3.raw[:r3]) == ac["sha256"]
+    # 65537 and 1 MiB against the oracle (pinned by the KATs above)
+    state = C.create_string_buffer(16416)
+    for n, content in ((65537, "comp"), (65537, "text"), (1 << 20, "comp"), (1 << 20, "rand"),
+                       (300000, "zeros")):
+        src = I.make(content, n, seed=n)
+        bound = product.compressBound(n)
+        er, eout = orc_compress(oracle, src)
+        out = C.create_string_buffer(bound + 64)
+        assert L.APE_LZ4_compress_default(buf(src), out, n, bound) == er
+        assert out.raw[:er] == eout, (n, content)
+        out2 = C.create_string_buffer(bound + 64)
+        assert L.APE_LZ4_compress_fast_extState(state, buf(src), out2, n, bound, 1) == er
+        assert out2.raw[:er] == eout
