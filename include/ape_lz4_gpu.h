@@ -170,6 +170,38 @@ int APE_LZ4_decompress_safe_batch_host(const char *const *h_src, const int *h_co
                                        char *const *h_dst, const int *h_maxDecompressedSize,
                                        int *h_result, int nblocks);
 
+/* ---- socket path (BASELINE config 5; lz4_sock.hip) ----
+ * APE_LZ4_rxbuf: the receive buffer of ape_socket (`buffer`, ref src/ape_buffer.c:210-228)
+ * as a growable host buffer registered with hipHostRegister, plus a frame parser for the
+ * [le32 size][block] stream that is correct across any read boundaries (the reference's
+ * parser desyncs, src/ape_socket.c:1372-1379).
+ *   rxbuf_prepare(b, n) : >= n free bytes after `used` (realloc + re-register); 0 / -1
+ *   rxbuf_append        : copy bytes in (what a read() into data + used does)
+ *   rxbuf_frames        : off[0..n) = complete frames' header positions, off[n] = their end;
+ *                         returns n (<= max_frames), or -1 for a size < 0 or > max_block
+ *   rxbuf_consume(b, k) : drop the first k bytes
+ * socket_send_blocks : nblocks host blocks -> GPU encode -> frames -> write(fd); returns the
+ *                      bytes written or an APE_LZ4_GPU_E* code.
+ * socket_recv_blocks : read(fd) -> rxbuf -> GPU decode from the frames -> host blocks;
+ *                      h_result[i] as decompress_safe; returns the blocks received, or an
+ *                      APE_LZ4_GPU_E* code (EINVAL also for a malformed stream / early EOF).
+ * Both are blocking calls for one connection; each overlaps socket I/O with GPU work. */
+typedef struct APE_LZ4_rxbuf APE_LZ4_rxbuf;
+APE_LZ4_rxbuf *APE_LZ4_rxbuf_new(size_t initial);
+int APE_LZ4_rxbuf_prepare(APE_LZ4_rxbuf *b, size_t more);
+int APE_LZ4_rxbuf_append(APE_LZ4_rxbuf *b, const char *data, size_t len);
+int APE_LZ4_rxbuf_frames(const APE_LZ4_rxbuf *b, long long *off, int max_frames, int max_block);
+void APE_LZ4_rxbuf_consume(APE_LZ4_rxbuf *b, size_t n);
+char *APE_LZ4_rxbuf_data(APE_LZ4_rxbuf *b);
+size_t APE_LZ4_rxbuf_used(const APE_LZ4_rxbuf *b);
+size_t APE_LZ4_rxbuf_room(const APE_LZ4_rxbuf *b);
+int APE_LZ4_rxbuf_pinned(const APE_LZ4_rxbuf *b);
+void APE_LZ4_rxbuf_free(APE_LZ4_rxbuf *b);
+long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_stride, int block_size,
+                                     int nblocks, int batch);
+long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int block_size,
+                                     int nblocks, int batch, int *h_result);
+
 /* ---- synthetic benchmark data, device-side ----
  * kind 0 = random bytes, 1 = compressible; block b is seeded with first_block+b. */
 int APE_LZ4_synth_blocks_dev(char *d_out, size_t stride, int blockSize,

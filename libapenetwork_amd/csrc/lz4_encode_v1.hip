@@ -1,0 +1,949 @@
+// lz4_encode_v1.hip -- the round-1 encoder, kept for A/B measurement only
+// (APE_LZ4_ENCODER=v1 selects it; lz4_encode.hip is the product encoder).
+//
+// Replaces the per-block work of APE_LZ4_compress_default (ref src/ape_lz4.c:
+// 811-815 -> LZ4_compress_generic :530-755, byU16 / noDict).  The output is a
+// valid LZ4 v1.7.1 block -- it obeys every parsing rule decompress_safe enforces
+// (:1346-1366, :1375, :1444-1447): matches start at <= n-12, end at <= n-5, the
+// last >= 5 bytes are literals -- but it is produced by a chunk-parallel parse,
+// not by the reference's sequential search, so the bytes differ.
+//
+// One 192-thread workgroup (three waves, one role each) per block; a batch holds
+// ~1M blocks, so most of the parallelism comes from many blocks in flight (8 per
+// CU).  Per block the LDS (20.0 KiB) holds the reference's own hash table (8192 x
+// u16, 13-bit hash of 5 bytes, :449-462), a 1 KiB ring of recent input and the
+// hand-over records between the roles.  The input stays in HBM/L2.
+//
+// The block is cut into chunks of 64 positions, one per lane.  The waves run in
+// lock step, two workgroup barriers per step s (each waits only on its own memory
+// operations; s_waitcnt vmcnt counts a wave's loads and stores together, in order):
+//   PRODUCER (wave 1), three chunks in flight:
+//     A(s+3)  load in[p, p+8) for every position p of the chunk;
+//     B(s+2)  hash in[p, p+5), read candidate T = table[h] (positions walked
+//             earlier plus match_end - 2, inserted as the reference does:
+//             :595-619, :680-706) and L = the earliest lane of the chunk with the
+//             same hash bits; copy the chunk into the ring; load in[T-4, T+28);
+//     C1(s+1) verify 4 bytes for T and L, measure both to 28 bytes forward and 4
+//             backward, keep the longer (then closer); load 32 more for a 28;
+//     C2(s)   (second half) finish those to 60 bytes, hash match_end - 2 ->
+//             match info of chunk s in LDS.
+//   WALKER (wave 0), chunk s-1: the greedy chain on the scalar unit (hops over the
+//     match lanes of a ballot mask), catch-up into pending literals (:623-627),
+//     the wave-wide extension of matches >= 60 bytes; second half: table inserts
+//     of the walked positions and match_end - 2 (:680), never overlapping B.
+//   EMITTER (wave 2), chunk s-2: sizes and prefix-sum offsets of the sequences,
+//     then each lane of a 64-byte output window computes its output byte; the
+//     last literals (:732-751) are copied with 16-byte moves.
+#include "lz4_gpu_internal.h"
+#include <type_traits>
+
+namespace apelz4 {
+
+#ifdef APE_LZ4_STATS
+__device__ unsigned long long g_enc_stats_v1[16];
+#endif
+
+namespace {
+
+#ifndef APE_LZ4_HLOG
+#define APE_LZ4_HLOG 13
+#endif
+constexpr int kHLog = APE_LZ4_HLOG;
+constexpr int kHSize = 1 << kHLog;
+constexpr uint32_t kEagerLen = 28;   // match bytes measured by the producer (T candidate)
+constexpr uint32_t kEagerL = 12;     // ... for the in-chunk candidate L
+#ifndef APE_LZ4_ERING
+#define APE_LZ4_ERING 1024
+#endif
+constexpr uint32_t kRingE = APE_LZ4_ERING;  // recent input bytes (own, stage 2, end-2, literals)
+#ifndef APE_LZ4_SCRBITS
+#define APE_LZ4_SCRBITS 6
+#endif
+constexpr uint32_t kScr = 1u << APE_LZ4_SCRBITS;  // in-chunk candidate scratch entries
+constexpr int kSmall = 128;          // smaller blocks take the byte-load path
+
+
+// info.x: len (8) | back << 8 (3) | trunc << 11 | has << 12 | hashable << 13 |
+//         e2 << 14 | hash(match_end - 2) << 16;   info.y: offset | h << 16
+constexpr uint32_t I_TRUNC = 1u << 11, I_HAS = 1u << 12, I_HASHABLE = 1u << 13,
+                   I_E2 = 1u << 14;
+
+struct __attribute__((aligned(16))) EncLds {
+    uint16_t tab[kHSize];
+    // input byte x at ring byte (x mod kRingE); the first 64 bytes are mirrored
+    // after the end, so a 36-byte read never wraps (immediate LDS offsets)
+    uint32_t ring[kRingE / 4 + 16];
+    uint2 info[3][64];               // producer -> walker and emitter, chunk k in [k % 3]
+    uint32_t scr[kScr];              // producer scratch: earliest lane per low hash bits
+    uint2 wres[2][64];               // walker -> emitter: {m_len | m_back << 20, anchor}
+    uint32_t wmem[2][2];             // walker -> emitter: member mask of the chunk
+    uint32_t wend;                   // walker -> emitter: final anchor (last literals)
+    uint32_t omap[16];               // emitter: owner map of a 64-byte output window
+};
+
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt at their maxima = no wait).  The
+// producer states its pipeline's waits explicitly: the compiler's own counter
+// analysis treats a load whose consumer sits in a skipped branch as still in flight
+// and then waits for every load before the register is reused.
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    static_assert(N >= 0 && N < 16, "vmcnt");
+    __builtin_amdgcn_s_waitcnt(N | (7 << 4) | (15 << 8));
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// X = L shifted by d bytes (X byte i = L byte i + d, 0 outside L), |d| < 32,
+// with compile-time register indices only (a barrel shifter).
+__device__ __forceinline__ void shift_bytes(const uint32_t (&L)[8], int d, uint32_t (&X)[8]) {
+    uint32_t T[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) T[k] = L[k];
+    const bool down = d >= 0;
+    const int ad = down ? d : -d, w = ad >> 2;
+    const uint32_t r = (uint32_t)ad & 3u;
+#pragma unroll
+    for (int bit = 4; bit >= 1; bit >>= 1) {
+        if (w & bit) {
+            if (down) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) T[k] = (k + bit < 8) ? T[k + bit] : 0u;
+            } else {
+#pragma unroll
+                for (int k = 7; k >= 0; k--) T[k] = (k - bit >= 0) ? T[k - bit] : 0u;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (down) X[k] = __builtin_amdgcn_alignbyte(k + 1 < 8 ? T[k + 1] : 0u, T[k], r);
+        else X[k] = r ? __builtin_amdgcn_alignbyte(T[k], k >= 1 ? T[k - 1] : 0u, 4u - r) : T[k];
+    }
+}
+
+// 32 bytes in[pos, pos+32) (bytes outside [0, n) read as 0).
+// SMALL: byte loads.  Otherwise (n >= 32): two unaligned 16-byte loads from the
+// clamped window, fixed up with ALU only (so the wave's vmcnt accounting stays
+// static in the pipelined loop).
+// fast (wave-uniform): every lane's window is known to lie inside [0, n).
+template <bool SMALL>
+__device__ __forceinline__ void load32(gcu8 *in, int n, int pos, uint32_t (&X)[8],
+                                       bool fast = false) {
+    if (!SMALL && fast) {
+        gcu8 *q = in + (uint32_t)pos;   // saddr + voffset, +16 as the immediate offset
+        const uint4 a = gload16(q), b = gload16(q + 16);
+        X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w;
+        X[4] = b.x; X[5] = b.y; X[6] = b.z; X[7] = b.w;
+        return;
+    }
+    if (SMALL) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) X[k] = 0;
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+            const int q = pos + k;
+            if (q >= 0 && q < n) X[k >> 2] |= (uint32_t)in[(uint32_t)q] << (8 * (k & 3));
+        }
+        return;
+    }
+    const int ca = pos < 0 ? 0 : (pos > n - 32 ? n - 32 : pos);
+    gcu8 *q = in + (uint32_t)ca;
+    const uint4 a = gload16(q), b = gload16(q + 16);
+    const uint32_t L[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    if (ca == pos) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) X[k] = L[k];
+    } else {
+        // the clamped window ends at n / starts at 0, so shifting it zero-fills
+        // exactly the bytes outside [0, n)
+        const int d = pos - ca;   // |d| >= 32 only for lanes past the block end
+        shift_bytes(L, d < -31 ? -31 : (d > 31 ? 31 : d), X);
+        if (d > 31 || d < -31) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) X[k] = 0;
+        }
+    }
+}
+
+// Hash of the 5 bytes at p (x1 = in[p..p+3], b4 = in[p+4]) into kHLog bits.  The
+// reference multiplies the 40-bit sequence by 889523592379 (:456-473), which needs
+// quarter-rate 32-bit multiplies here; any hash gives a valid stream, so this one
+// uses two full-rate 24 x 24-bit multiplies (v_mul_u32_u24) of bytes 0-2 and
+// bytes 3-4.  Same ratio on the App. C data (tools/enc_model.c: 3.1613 vs 3.1600).
+__device__ __forceinline__ uint32_t hash5(uint32_t x1, uint32_t b4) {
+    const uint32_t lo = x1 & 0xFFFFFFu, hi = (x1 >> 24) | ((b4 & 0xFFu) << 8);
+    // (__umul24 returns int: do the sum and the shift unsigned)
+    return ((uint32_t)__umul24(lo, 0x9E3779u) + (uint32_t)__umul24(hi, 0xC2B2AEu)) >> (32 - kHLog);
+}
+
+// v_ffbl_b32 / v_ffbh_u32: lowest / highest set bit, 0xFFFFFFFF for 0 (inline asm
+// so that the compiler does not turn the zero case into compare + select)
+__device__ __forceinline__ uint32_t ffbl(uint32_t d) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(d));
+    return r;
+}
+__device__ __forceinline__ uint32_t ffbh(uint32_t d) {
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(d));
+    return r;
+}
+
+// first differing bit of dwords A[K0..K1) vs B (bit index from A[K0]'s bit 0), or
+// 0xFFFFFFFF: ffbl + saturating add + min3 per dword, no compares or selects
+template <int K0, int K1>
+__device__ __forceinline__ uint32_t first_diff_bit(const uint32_t (&A)[8], const uint32_t (&B)[8]) {
+    uint32_t m = ffbl(A[K0] ^ B[K0]);
+#pragma unroll
+    for (int k = K0 + 1; k < K1; k++)
+        m = umin(m, __builtin_elementwise_add_sat(ffbl(A[k] ^ B[k]), 32u * (uint32_t)(k - K0)));
+    return m;
+}
+
+// common length of X and Y from byte 4 (dword 1) on, up to kEagerLen
+__device__ __forceinline__ uint32_t eager(const uint32_t (&X)[8], const uint32_t (&Y)[8]) {
+    return umin((first_diff_bit<2, 8>(X, Y) >> 3) + 4u, kEagerLen);
+}
+
+// bytes equal just before the match (in[p-1] == in[c-1], ...), 0..4
+__device__ __forceinline__ uint32_t back4(uint32_t x0, uint32_t y0) {
+    return umin(ffbh(x0 ^ y0) >> 3, 4u);
+}
+
+// e / 255 with one full-rate 24-bit multiply: 255 * 0x8081 = 2^23 + 127, so
+// floor(e * 0x8081 / 2^23) = floor(e / 255) for e < 66060 (lengths here are < 65537)
+__device__ __forceinline__ uint32_t div255(uint32_t e) {
+    return (uint32_t)__umul24(e, 0x8081u) >> 23;
+}
+
+// bytes after a 15 nibble: v < 15 -> 0, else (v - 15) / 255 + 1 -- both are
+// (v + 240) / 255 (v + 240 < 255 below 15; one full-rate multiply, no select)
+__device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {
+    return div255(v + 240u);
+}
+
+// write the length extension of v (>= 15) at o
+__device__ __forceinline__ void put_len(gu8 *o, uint32_t v) {
+    if (v < 15) return;
+    v -= 15;
+    uint32_t k = 0;
+    for (; v >= 255; v -= 255) o[k++] = 255;
+    o[k] = (uint8_t)v;
+}
+
+// 4 input bytes at x from the ring
+__device__ __forceinline__ uint32_t ring4(const EncLds &S, uint32_t x) {
+    const uint32_t *r = S.ring + ((x >> 2) & (kRingE / 4 - 1));
+    return __builtin_amdgcn_alignbyte(r[1], r[0], x & 3u);
+}
+
+// 32 input bytes at x from the ring
+__device__ __forceinline__ void ring32(const EncLds &S, uint32_t x, uint32_t (&O)[8]) {
+    const uint32_t *r = S.ring + ((x >> 2) & (kRingE / 4 - 1));
+    const uint32_t sh = x & 3u;
+    uint32_t W[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) W[k] = r[k];
+#pragma unroll
+    for (int k = 0; k < 8; k++) O[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
+}
+
+// Copy in[a, a+len) to dst[o, o+len) with the whole wave (16 bytes per lane per step).
+__device__ __forceinline__ void wave_copy(gcu8 *in, gu8 *dst, uint32_t a, uint32_t o,
+                                          uint32_t len, int lane) {
+    for (uint32_t k = 16u * (uint32_t)lane; k < len; k += 1024u) {
+        if (k + 16u <= len) {
+            gstore16(dst + (o + k), gload16(in + (a + k)));
+        } else {
+            for (uint32_t t = k; t < len; t++) dst[o + t] = in[a + t];
+        }
+    }
+}
+
+struct Blk {
+    gcu8 *in;
+    gu8 *dst;
+    int n;
+    uint32_t un, cap, mstart, mlimit;
+    int nch;                         // chunks of 64 positions
+    int k0;                          // first chunk to encode: positions [0, 64 k0) are the
+                                     // history prefix (withPrefix encode), only hashed
+    uint32_t nr;                     // bytes to encode (n - 64 k0)
+    bool noL;                        // acceleration > 1: no in-chunk candidate
+};
+
+// ---------------- producer ----------------
+struct Part {                        // C1 result of one chunk, finished by C2
+    uint32_t len, c, bk, lim, h, base;   // base: bytes C1 measured (kEagerLen / kEagerL)
+    bool has, hashable, trunc1;
+};
+
+// One parity of the producer pipeline (the step loop is unrolled by two, so no
+// register set is ever copied): X from A for B, Y/cT/jL/h from B for C1, q/E from
+// C1 for C2.
+struct PSet {
+    uint32_t X[2];                   // own bytes in[p, p+8) of the chunk B works on next
+    uint32_t Y[8];                   // T-candidate bytes
+    uint32_t E[8];                   // second-stage candidate bytes
+    uint32_t cT, jL, h;
+    Part q;
+};
+
+// A(k): own bytes in[p, p+8) for the hash (0 past the block end)
+template <bool SMALL, bool FAST = false>
+__device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_t (&X)[2]) {
+    const uint32_t pos = (k < B.nch ? 64u * (uint32_t)k : 0u) + (uint32_t)lane;
+    if (FAST || (!SMALL && 64 * k + 72 <= B.n)) {   // wave-uniform: the whole window is inside
+        const uint2 v = gload8(B.in + pos);
+        X[0] = v.x;
+        X[1] = v.y;
+        return;
+    }
+    X[0] = X[1] = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < 8u; t++)
+        if (pos + t < B.un) X[t >> 2] |= (uint32_t)B.in[pos + t] << (8 * (t & 3));
+}
+
+// T candidate bytes of chunk k (issued one step before C1 consumes them).  Candidates
+// below position 4 are skipped: their 4 bytes of backward context would start before
+// the block and need the slow edge path (never-written slots read as 0).
+template <bool SMALL, bool FAST = false>
+__device__ __forceinline__ void prod_fetch_t(const Blk &B, int k, int lane, uint32_t cT,
+                                             uint32_t (&Y)[8]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const bool tryT = k < B.nch && cT < p && cT >= 4u;
+    load32<SMALL>(B.in, B.n, tryT ? (int)cT - 4 : 0, Y, FAST || 64 * k + 91 <= B.n);
+}
+
+// B(k): hash, table + in-chunk candidates, T fetch issue, ring copy
+template <bool SMALL, bool FAST = false>
+__device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int lane,
+                                            const uint32_t (&X)[2], uint32_t &cT, uint32_t &jL,
+                                            uint32_t &h, uint32_t (&Y)[8]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const bool live = k < B.nch;
+    const bool hashable = live && p + 5u <= B.un;
+    h = hash5(X[0], X[1]);
+    cT = S.tab[h];
+    jL = 0xFFFFFFFFu;
+    if (!B.noL) {   // wave-uniform
+        const uint32_t hs = h & (kScr - 1u);
+        if (hashable) atomicMin(&S.scr[hs], (uint32_t)lane);
+        wave_sync();
+        jL = hashable ? S.scr[hs] : 0xFFFFFFFFu;
+        wave_sync();
+        if (hashable) S.scr[hs] = 0xFFFFFFFFu;
+    }
+    // ring copy of this chunk (own bytes for C1, second stage, match_end - 2,
+    // literals); zero past the block end
+    if (live) {
+        const uint8_t by = (uint8_t)X[0];
+        ((uint8_t *)S.ring)[p & (kRingE - 1)] = by;
+        if (((64u * (uint32_t)k) & (kRingE - 1)) == 0u) ((uint8_t *)S.ring)[kRingE + lane] = by;
+    }
+    // T candidate bytes (issued now, consumed one step later).  Candidates below
+    // position 4 are skipped: their 4 bytes of backward context would start before
+    // the block and need the slow edge path (never-written slots read as 0).
+    prod_fetch_t<SMALL, FAST>(B, k, lane, cT, Y);
+}
+
+// C1(k): verify / measure 28 bytes / pick; issue the second-stage load
+template <bool SMALL, bool FAST = false>
+__device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int k, int lane,
+                                             const uint32_t (&Y)[8], uint32_t cT, uint32_t jL,
+                                             uint32_t h, Part &R, uint32_t (&E)[8]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    uint32_t X[8];
+    ring32(S, p - 4u, X);            // own bytes in[p-4, p+28) (ring tail = 0 before 0)
+    const bool live = k < B.nch;
+    R.hashable = live && p + 5u <= B.un;
+    const bool can = live && p >= 1u && p <= B.mstart && B.n >= kMinLength;
+    const uint32_t cL = 64u * (uint32_t)k + jL;
+    // L candidate bytes in[cL-4, cL+12) from lane jL's own bytes
+    uint32_t Z[8];
+#pragma unroll
+    for (int t = 0; t < 4; t++) Z[t] = (uint32_t)__shfl((int)X[t], (int)(jL & 63u), 64);
+#pragma unroll
+    for (int t = 4; t < 8; t++) Z[t] = 0u;
+    const bool okT = can && cT < p && cT >= 4u && Y[1] == X[1];
+    const bool okL = can && jL < (uint32_t)lane && cL != cT && Z[1] == X[1];   // jL = ~0 if noL
+    R.lim = can ? B.mlimit - p : 0u;
+    // measured unconditionally (selects, no branches): every lane reads Y, so the
+    // compiler sees the candidate load consumed on every path.  T to 28 bytes, L to 12:
+    // L (the closer one) is taken when T is shorter than 12 and L at least as long,
+    // and C2 continues the taken candidate from where C1 stopped
+    // (tools/enc_model.c model4, pol 7 vs 0: ratio -0.1 %; measured -0.06 %, -3.4 % VALU).
+    const uint32_t eT = eager(X, Y);
+    const uint32_t eL = umin((first_diff_bit<2, 4>(X, Z) >> 3) + 4u, kEagerL);
+    const uint32_t lT = okT ? eT : 0u, lL = okL ? eL : 0u;
+    const bool pickL = okL && (!okT || (lT < kEagerL && lL >= lT));
+    R.c = pickL ? cL : cT;
+    R.len = pickL ? lL : lT;
+    R.base = pickL ? kEagerL : kEagerLen;
+    R.trunc1 = R.len >= R.base && R.lim > R.base;
+    if (R.len > R.lim) R.len = R.lim;
+    R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
+    R.has = okT || okL;
+    R.h = h;
+    load32<SMALL>(B.in, B.n, R.trunc1 ? (int)(R.c + R.base) : 0, E,
+                  FAST || 64 * k + 123 <= B.n);
+}
+
+// C2(k): finish the truncated lengths against the ring, hash match_end - 2 -> info
+__device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int lane,
+                                            const Part &R, const uint32_t (&E)[8]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    uint32_t len = R.len;
+    bool trunc = false;
+    {   // unconditional for the same reason as in C1
+        uint32_t O[8];
+        ring32(S, p + R.base, O);                // own bytes p+base .. p+base+32
+        const uint32_t ext = umin(first_diff_bit<0, 8>(O, E) >> 3, 32u);
+        if (R.trunc1) {
+            len = umin(R.base + ext, R.lim);
+            trunc = ext == 32u && R.lim > R.base + 32u;
+        }
+    }
+    uint32_t e2 = 0;
+    if (R.has && !trunc) {
+        const uint32_t at = p + len - 2u;         // match end - 2 (:680)
+        if (at + 5u <= B.un) e2 = I_E2 | (hash5(ring4(S, at), ring4(S, at + 4u)) << 16);
+    }
+    S.info[k % 3][lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
+                                         (R.has ? I_HAS : 0u) | (R.hashable ? I_HASHABLE : 0u) | e2,
+                                     (R.has ? p - R.c : 0u) | (R.h << 16));
+}
+
+// ---------------- walker ----------------
+struct Walk {
+    uint32_t q;          // walk position
+    uint32_t anchor;     // start of the pending literals
+};
+
+// forward extension of the match at m (candidate cm) from L bytes on, with the
+// whole wave, 1 KiB per step; returns the full length (<= mlimit - m)
+__device__ __forceinline__ uint32_t extend_match(const Blk &B, uint32_t m, uint32_t cm, uint32_t L,
+                                                 int lane) {
+    const uint32_t lm = B.mlimit - m;
+    for (;;) {
+        const uint32_t kk = L + 16u * (uint32_t)lane;
+        uint32_t d = 0, at = 0;
+        if (kk < lm) {
+            uint32_t xb[4] = {0, 0, 0, 0}, yb[4] = {0, 0, 0, 0};
+            if (m + kk + 16u <= B.un) {
+                const uint4 x = gload16(B.in + (m + kk)), y = gload16(B.in + (cm + kk));
+                xb[0] = x.x; xb[1] = x.y; xb[2] = x.z; xb[3] = x.w;
+                yb[0] = y.x; yb[1] = y.y; yb[2] = y.z; yb[3] = y.w;
+            } else {
+#pragma unroll
+                for (uint32_t t = 0; t < 16u; t++) {
+                    if (m + kk + t < B.un) {
+                        xb[t >> 2] |= (uint32_t)B.in[m + kk + t] << (8 * (t & 3));
+                        yb[t >> 2] |= (uint32_t)B.in[cm + kk + t] << (8 * (t & 3));
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 3; t >= 0; t--) {
+                const uint32_t e = xb[t] ^ yb[t];
+                if (e) { d = 1; at = 4u * (uint32_t)t + (__builtin_ctz(e) >> 3); }
+            }
+        }
+        const uint64_t bad = wave_ballot(d != 0 || kk >= lm);
+        if (bad) {
+            const int fl = __builtin_ctzll(bad);
+            const uint32_t k2 = L + 16u * (uint32_t)fl;
+            L = k2 >= lm ? lm : k2 + lane_val(at, fl);
+            break;
+        }
+        L += 1024u;
+    }
+    return L > lm ? lm : L;
+}
+
+// Walk chunk k (first half of step k + 1), then (second half) insert the walked
+// positions and match_end - 2 into the table and hand the members to the emitter.
+// The greedy chain (:591-627: a position with a match jumps past it, any other
+// position is a literal): the scalar unit hops over the match lanes only (ballot
+// mask, one v_readlane per member); walked positions, catch-up limits (:623-627)
+// and the new anchor follow for all 64 lanes at once from the member set.  A match
+// the producer could not finish (TRUNC, >= 60 bytes) is extended by the whole wave.
+struct WalkOut {
+    uint64_t walked, members;
+    uint32_t m_back, m_len, an;   // per member lane
+    uint2 iv;
+    uint32_t q0, Lf;              // walk start; forward match length per lane
+};
+
+// First half: the hop chain only (the latency-bound part); second half, before the
+// inserts: the lane-parallel catch-up limits, walked set and anchor (walk_finish).
+__device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k, int lane, Walk &W,
+                                           WalkOut &O) {
+    const uint32_t P = 64u * (uint32_t)k;
+    O.walked = O.members = 0;
+    O.m_back = O.m_len = O.an = 0;
+    O.iv = S.info[k % 3][lane];
+    O.q0 = W.q;
+    O.Lf = O.iv.x & 0xFFu;                               // forward match length
+    if (W.q >= P + 64u) return;               // a match from earlier chunks covers it
+    const uint2 iv = O.iv;
+    const bool has = (iv.x & I_HAS) != 0u, trunc = (iv.x & I_TRUNC) != 0u;
+    const uint64_t Hm = wave_ballot(has);
+    const uint32_t Lh = has ? (trunc ? 0x80u : O.Lf) : 0u;   // hop; 0x80 = unfinished
+    uint32_t rel = W.q - P;
+    uint64_t M = 0;
+    for (;;) {
+        const uint64_t w = Hm >> rel;
+        if (w == 0) { rel = 64u; break; }
+        const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
+        const uint32_t h = lane_val(Lh, (int)j);
+        M |= 1ull << j;
+        if (h & 0x80u) {
+            const uint32_t me = P + j;
+            const uint32_t cm = me - (lane_val(iv.y, (int)j) & 0xFFFFu);
+            const uint32_t Le = extend_match(B, me, cm, lane_val(iv.x, (int)j) & 0xFFu, lane);
+            if ((uint32_t)lane == j) O.Lf = Le;
+            rel = j + Le;
+        } else {
+            rel = j + h;
+        }
+        if (rel >= 64u) break;
+    }
+    O.members = M;
+    W.q = P + rel;
+}
+
+__device__ __forceinline__ void walk_finish(int k, int lane, Walk &W, WalkOut &O) {
+    const uint32_t P = 64u * (uint32_t)k;
+    if (O.q0 >= P + 64u) return;              // covered by a match from earlier chunks
+    // catch-up limits: a member's backward extension stops at the previous end
+    const uint32_t anchor0 = W.anchor;
+    const bool mem = (O.members >> lane) & 1ull;
+    const uint32_t p = P + (uint32_t)lane;
+    const uint32_t end = mem ? p + O.Lf : 0u;
+    const uint32_t imax = wave_incl_max(end);
+    const uint32_t pm = umax(wave_shr1(imax, 0u), anchor0);
+    const uint32_t bk = umin((O.iv.x >> 8) & 7u, p - pm);
+    O.m_back = bk;
+    O.m_len = O.Lf + bk;
+    O.an = pm;
+    // walked = every position from the walk start that no match of this chunk covers
+    O.walked = wave_ballot(p >= umax(O.q0, pm));
+    W.anchor = umax(anchor0, lane_val(imax, 63));
+}
+
+__device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int lane,
+                                             const WalkOut &O) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const uint2 iv = O.iv;
+    if (((O.walked >> lane) & 1ull) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
+    const bool mem = (O.members >> lane) & 1ull;
+    const uint32_t fwd = O.m_len - O.m_back;      // match length from p
+    // match_end - 2 (:680): hashed by the producer unless the walker extended the match
+    uint32_t e2h = (iv.x >> 16) & (kHSize - 1);
+    bool e2ok = mem && (iv.x & I_E2) && !(iv.x & I_TRUNC);
+    if (mem && (iv.x & I_TRUNC)) {
+        const uint32_t e2 = p + fwd - 2u;
+        if (e2 + 5u <= B.un) {
+            uint32_t lo32 = 0, b4 = 0;
+            for (uint32_t t = 0; t < 5u; t++) {
+                const uint32_t by = B.in[e2 + t];
+                if (t < 4) lo32 |= by << (8 * t); else b4 = by;
+            }
+            e2h = hash5(lo32, b4);
+            e2ok = true;
+        }
+    }
+    // one wave's LDS operations complete in order: the walked-position inserts above
+    // land before these (compiler barrier only)
+    __builtin_amdgcn_sched_barrier(0);
+    if (e2ok) S.tab[e2h] = (uint16_t)(p + fwd - 2u);
+    S.wres[k & 1][lane] = make_uint2(O.m_len | (O.m_back << 20), O.an);
+    if (lane == 0) {
+        S.wmem[k & 1][0] = (uint32_t)O.members;
+        S.wmem[k & 1][1] = (uint32_t)(O.members >> 32);
+    }
+}
+
+// ---------------- emitter ----------------
+// Chunks are emitted in pairs (one 64-byte output window holds ~40 bytes of two
+// chunks' sequences instead of ~20 of one): sizes of each chunk in the second half
+// of step k + 2, both chunks' bytes in the first half of step kA + 4 (kA = the pair's
+// first chunk).
+struct EmitC {          // one chunk's sequences, per member lane
+    uint64_t members;
+    uint32_t tot, ex, an, lit, mo;
+};
+struct Emit {
+    uint32_t o;          // output cursor
+    bool overflow;
+    bool pend;           // A (and B) prepared, not yet written
+    int kA;              // first chunk of the pending pair
+    EmitC A, Bc;
+};
+
+// Sizes and output offsets of chunk k's sequences into C; `before` = output bytes of
+// the pair's earlier chunk.
+__device__ __forceinline__ void emit_prepare(const EncLds &S, const Blk &B, int k, int lane, Emit &E,
+                                             EmitC &C, uint32_t before) {
+    C.tot = 0;
+    const uint64_t members = ((uint64_t)__builtin_amdgcn_readfirstlane(S.wmem[k & 1][1]) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane(S.wmem[k & 1][0]);
+    C.members = E.overflow ? 0ull : members;
+    if (!C.members) return;
+    const uint2 wr = S.wres[k & 1][lane];
+    const uint32_t off = S.info[k % 3][lane].y & 0xFFFFu;
+    const bool mem = (C.members >> lane) & 1ull;
+    const uint32_t m_len = wr.x & 0xFFFFFu, m_back = wr.x >> 20;
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const uint32_t ms = p - m_back;            // match start after catch-up
+    C.an = wr.y;
+    C.lit = mem ? ms - C.an : 0u;
+    const uint32_t ml = m_len - kMinMatch;
+    const uint32_t size = mem ? 1u + ext_bytes(C.lit) + C.lit + 2u + ext_bytes(ml) : 0u;
+    C.ex = wave_excl_scan(size);
+    C.tot = lane_val(C.ex + size, 63);
+    C.mo = ml | (off << 16);
+    if ((uint64_t)E.o + before + C.tot > B.cap) {
+        E.overflow = true;
+        C.members = 0;
+        C.tot = 0;
+    }
+}
+
+// Gather the pair (kA, kA + 1).  Lane L of window w produces output byte w + L; its
+// sequence is the last member starting at or before it (owner map + prefix max over
+// owners 1..64 = chunk A's lanes, 65..128 = chunk B's, B's all after A's), whose
+// record comes over by ds_bpermute.  One wave's LDS operations complete in order, so
+// the owner-map writes, the read-back and the clearing need no waits.
+__device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int kA, int lane, Emit &E) {
+    const uint32_t totA = E.A.tot, tot = totA + E.Bc.tot;
+    if (tot == 0) return;
+    const uint32_t P = 64u * (uint32_t)kA;
+    // runs in the first half of step kA + 4, while the producer copies chunk kA + 6
+    // into the ring (or after the last step): input [rlo, P + 384) is intact there
+    const uint32_t rlo = P + 448u > kRingE ? P + 448u - kRingE : 0u;
+    const bool memA = (E.A.members >> lane) & 1ull, memB = (E.Bc.members >> lane) & 1ull;
+    const uint32_t exA = E.A.ex, exB = totA + E.Bc.ex;
+    // member starts, ~0 for other lanes: the window tests below are single compares
+    const uint32_t sA = memA ? exA : 0xFFFFFFFFu, sB = memB ? exB : 0xFFFFFFFFu;
+    gu8 *out = B.dst + E.o;
+    for (uint32_t w = 0; w < tot; w += 64u) {
+        const bool markA = sA - w - 1u < 63u;    // w < start < w + 64
+        const bool markB = sB - w - 1u < 63u;
+        if (markA) ((uint8_t *)S.omap)[exA - w] = (uint8_t)(lane + 1);
+        if (markB) ((uint8_t *)S.omap)[exB - w] = (uint8_t)(lane + 65);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t mk = ((const uint8_t *)S.omap)[lane];
+        __builtin_amdgcn_sched_barrier(0);
+        if (markA) ((uint8_t *)S.omap)[exA - w] = 0;
+        if (markB) ((uint8_t *)S.omap)[exB - w] = 0;
+        const uint64_t covA = wave_ballot(sA <= w);   // member 0 of A starts at 0
+        const uint64_t covB = wave_ballot(sB <= w);
+        const uint32_t carry = covB ? 128u - (uint32_t)__clzll((long long)covB)
+                                    : 64u - (uint32_t)__clzll((long long)covA);
+        const uint32_t own = umax(wave_incl_max(mk), carry) - 1u;
+        const int sl = (int)((own & 63u) << 2);
+        const bool fb = own >= 64u;
+        // all eight permutes by every lane (a permute reads its source lane's register,
+        // so it must not run under a lane-dependent condition), then a select
+        const uint32_t a_ex = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)exA);
+        const uint32_t b_ex = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)exB);
+        const uint32_t a_an = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.an);
+        const uint32_t b_an = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.an);
+        const uint32_t a_li = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.lit);
+        const uint32_t b_li = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.lit);
+        const uint32_t a_mo = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.mo);
+        const uint32_t b_mo = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.mo);
+        const uint32_t r_ex = fb ? b_ex : a_ex, r_an = fb ? b_an : a_an;
+        const uint32_t rl = fb ? b_li : a_li, r_mo = fb ? b_mo : a_mo;
+        const uint32_t b = w + (uint32_t)lane;
+        // every candidate value computed, then selected (no divergent branches)
+        const uint32_t rr = b - r_ex;                    // offset inside the sequence
+        const uint32_t rml = r_mo & 0xFFFFu, roff = r_mo >> 16;
+        const uint32_t lit_at = 1u + ext_bytes(rl), off_at = lit_at + rl;
+        const uint32_t a = r_an + (rr - lit_at);         // literal source position
+        uint32_t v = ((const uint8_t *)S.ring)[a & (kRingE - 1)];
+        if (rr >= lit_at && rr < off_at && a < rlo) v = B.in[a];   // older than the ring (rare)
+        // length extension bytes: 255 while more than 254 remain, then the rest
+        // (the i-th byte after the nibble is min(255, v - 15 - 255 i))
+        const uint32_t vl = umin(rl - 15u - (uint32_t)__umul24(rr - 1u, 255u), 255u);
+        const uint32_t vm = umin(rml - 15u - (uint32_t)__umul24(rr - off_at - 2u, 255u), 255u);
+        const uint32_t vo = rr == off_at ? (roff & 0xFFu) : (roff >> 8);
+        v = rr < off_at ? v : (rr < off_at + 2u ? vo : vm);
+        v = rr < lit_at ? vl : v;
+        v = rr == 0u ? ((umin(rl, 15u) << 4) | umin(rml, 15u)) : v;
+        if (b < tot) out[b] = (uint8_t)v;
+    }
+    E.o += tot;
+}
+
+// ---------------- history prefix (withPrefix encode) ----------------
+// Positions [0, 64 k0) precede the block in memory (the previous <= 64 KiB of the
+// stream, as compress_fast_continue sees it, ref src/ape_lz4.c:1160-1220).  The
+// producer wave hashes every third of them into the table, as loadDict does
+// (:1127-1130; catch-up recovers the bytes a skipped start loses), oldest first (one
+// wave: its LDS writes land in order, so the newest position wins deterministically),
+// and copies the last 64 into the ring for the first chunk's backward context.
+__device__ __forceinline__ void prefix_history(EncLds &S, const Blk &B, int lane) {
+    const uint32_t D = 64u * (uint32_t)B.k0;
+    constexpr int kU = 8;   // loads in flight per trip (the loop is latency bound)
+    for (uint32_t v0 = 0; v0 < D; v0 += 192u * kU) {
+        uint2 x[kU];
+        bool ok[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t v = v0 + 192u * u + 3u * (uint32_t)lane;
+            ok[u] = v < D && v + 8u <= B.un;   // (the last few of a tiny block stay out)
+            x[u] = gload8(B.in + (ok[u] ? v : 0u));
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t v = v0 + 192u * u + 3u * (uint32_t)lane;
+            if (ok[u]) S.tab[hash5(x[u].x, x[u].y)] = (uint16_t)v;
+        }
+    }
+    const uint32_t p = D - 64u + (uint32_t)lane;
+    const uint8_t by = B.in[p];
+    ((uint8_t *)S.ring)[p & (kRingE - 1)] = by;
+    if (((D - 64u) & (kRingE - 1)) == 0u) ((uint8_t *)S.ring)[kRingE + lane] = by;
+}
+
+// ---------------- block ----------------
+// Three waves per block, one role each, in lock step (two barriers per step):
+//   step s, first half : producer A(s+3) B(s+2) C1(s+1) | walker walks s-1 | emitter writes
+//                                                         |   the pair (s-4, s-3) (every 2nd step)
+//   step s, second half: producer C2(s) -> info[s%3]     | walker inserts s-1, publishes
+//                                                         | emitter sizes s-2
+// Table inserts (second half) never overlap the producer's lookups (first half).
+template <bool SMALL>
+__device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, int lane,
+                                             int *result) {
+    STATS_DECL
+    const int k0 = B.k0;
+    const int nch = B.nr >= (uint32_t)kMinLength ? B.nch : k0;   // :584, shorter -> last literals only
+    const int nsteps = k0 + ((nch - k0 + 3) & ~1);   // >= nch + 2 steps (emission lags two)
+
+    // Each role runs its own loop (same barrier count: 1 + 2 per step), so the
+    // compiler's memory-counter waits in each loop see only that role's operations.
+    if (wave == 1) {
+        PSet P0, P1;
+        // one producer step; `cur` = set of parity s, `nxt` = parity s + 1
+        auto pstep = [&](auto fast, int s, PSet &cur, PSet &nxt) {
+            constexpr bool F = decltype(fast)::value;
+            // Every stage runs on every step, past the last chunk too (it then loads
+            // from the block start and records nothing), so the number of loads per
+            // step -- and with it the waits -- is the same on every path.
+            // In flight, oldest first: A(s+2), Y(s+1) x2, E(s) x2 -> A(s+2) at 4.
+            vm_wait<4>();
+            prod_load<SMALL, F>(B, s + 3, lane, nxt.X);
+            prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
+            // Y(s+1) x2, E(s) x2, A(s+3), Y(s+2) x2 -> Y(s+1) at 5
+            vm_wait<5>();
+            prod_measure<SMALL, F>(S, B, s + 1, lane, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q, nxt.E);
+            STAT(5);
+            __syncthreads();
+            STAT(6);
+            // E(s) x2, A(s+3), Y(s+2) x2, E(s+1) x2 -> E(s) at 5
+            vm_wait<5>();
+            prod_finish(S, B, s, lane, cur.q, cur.E);
+            STAT(7);
+            __syncthreads();
+            STAT(8);
+        };
+        if (k0 > 0) prefix_history(S, B, lane);
+        if (nch > k0) {  // prologue: A(k0), A(k0+1), B(k0), A(k0+2), B(k0+1), C1(k0)
+            prod_load<SMALL>(B, k0, lane, P0.X);
+            prod_load<SMALL>(B, k0 + 1, lane, P1.X);
+            prod_lookup<SMALL>(S, B, k0, lane, P0.X, P0.cT, P0.jL, P0.h, P0.Y);
+            prod_load<SMALL>(B, k0 + 2, lane, P0.X);
+            prod_lookup<SMALL>(S, B, k0 + 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
+            prod_measure<SMALL>(S, B, k0, lane, P0.Y, P0.cT, P0.jL, P0.h, P0.q, P0.E);
+        }
+        // nothing in flight at the loop entry, so the loop's counter waits depend only
+        // on its own issue order (once per block)
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        // Steps whose three loads all lie inside the block (A(s+3): 64(s+3)+72 <= n,
+        // Y(s+2): 64(s+2)+91, E(s+1): 64(s+1)+123) run a loop without the edge paths;
+        // the last few steps run the general one.
+        const int nfast_abs = SMALL ? 0 : (int)umin((uint32_t)(B.n >= 264 ? (B.n - 264) / 64 + 1 : 0),
+                                                    (uint32_t)nsteps);
+        const int nfast = nfast_abs > k0 ? k0 + ((nfast_abs - k0) & ~1) : k0;
+        int s = k0;
+        for (; s < nfast; s += 2) {   // no conditional step: see pstep
+            pstep(std::true_type{}, s, P0, P1);
+            pstep(std::true_type{}, s + 1, P1, P0);
+        }
+        for (; s < nsteps; s += 2) {
+            pstep(std::false_type{}, s, P0, P1);
+            pstep(std::false_type{}, s + 1, P1, P0);
+        }
+        STATS_FLUSH_TID(g_enc_stats_v1, 64);
+        return;
+    }
+    if (wave == 0) {   // walker: chunk s-1 during step s
+        Walk W;
+        W.q = 64u * (uint32_t)k0;
+        W.anchor = W.q;
+        WalkOut O;
+        __syncthreads();
+        for (int s = k0; s < nsteps; s++) {
+            const bool work = s >= k0 + 1 && s <= nch;
+            if (work) walk_chain(S, B, s - 1, lane, W, O);
+            STAT(0);
+            __syncthreads();
+            STAT(4);
+            if (work) {
+                walk_finish(s - 1, lane, W, O);
+                walk_publish(S, B, s - 1, lane, O);
+                STAT_ADD(11, __popcll(O.members));
+            }
+            if (s == nsteps - 1 && lane == 0) S.wend = W.anchor;
+            STAT(1);
+            STAT_ADD(10, 3);
+            __syncthreads();
+            STAT(3);
+        }
+        STATS_FLUSH(g_enc_stats_v1);
+        return;
+    }
+    // emitter: sizes of chunk s-2 in the second half of step s (the walker published it
+    // in step s-1); the bytes of a pair (kA, kA+1) in the first half of step kA+4 --
+    // next to the producer's and the walker's long first halves
+    Emit E;
+    E.o = 0;
+    E.overflow = false;
+    E.pend = false;
+    E.kA = k0;
+    E.A.members = E.Bc.members = 0;
+    E.A.tot = E.A.ex = E.A.an = E.A.lit = E.A.mo = 0;
+    E.Bc.tot = E.Bc.ex = E.Bc.an = E.Bc.lit = E.Bc.mo = 0;
+    __syncthreads();
+    for (int s = k0; s < nsteps; s++) {
+#ifdef APE_EXP_NOEMIT
+        const bool work = false;   // diagnostic: instruction count without the emitter
+#else
+        const bool work = true;
+#endif
+        const int r = s - k0;
+#ifdef APE_EMIT_SINGLE
+        if (work && E.pend && E.kA == s - 3) {   // diagnostic: one chunk per write
+            emit_write(S, B, s - 3, lane, E);
+            E.pend = false;
+        }
+#else
+        if (work && E.pend && E.kA == s - 4) {   // the pair prepared in steps s-2, s-1
+            emit_write(S, B, s - 4, lane, E);
+            E.pend = false;
+        }
+#endif
+        STAT(2);
+        __syncthreads();
+        STAT(14);
+        if (work && r >= 2 && s - 2 < nch) {
+#ifdef APE_EMIT_SINGLE
+            if (true) {
+#else
+            if (((r - 2) & 1) == 0) {            // first chunk of a pair
+#endif
+                E.Bc.members = 0;
+                E.Bc.tot = 0;
+                emit_prepare(S, B, s - 2, lane, E, E.A, 0u);
+                E.kA = s - 2;
+                E.pend = true;
+            } else {
+                emit_prepare(S, B, s - 2, lane, E, E.Bc, E.A.tot);
+            }
+        }
+        STAT(12);
+        __syncthreads();
+        STAT(15);
+    }
+    // the last pair may still be pending (its write step lies past the loop)
+    if (E.pend) emit_write(S, B, E.kA, lane, E);
+    // ---- last literals (:732-751), from the walker's final anchor ----
+    if (!E.overflow) {
+        const uint32_t anchor = S.wend;
+        const uint32_t lit = B.un - anchor;
+        const uint32_t hdr = 1u + ext_bytes(lit);
+        const uint32_t total = E.o + hdr + lit;
+        if (total > B.cap) {
+            E.overflow = true;
+        } else {
+            if (lane == 0) {
+                B.dst[E.o] = (uint8_t)((lit < 15u ? lit : 15u) << 4);
+                put_len(B.dst + E.o + 1, lit);
+            }
+            wave_copy(B.in, B.dst, anchor, E.o + hdr, lit, lane);
+            E.o = total;
+        }
+    }
+    if (lane == 0) *result = E.overflow ? 0 : (int)E.o;
+    STAT_ADD(13, 1);
+    STATS_FLUSH_TID(g_enc_stats_v1, 128);
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(6)))
+lz4_encode_v1_kernel(BlockArgs a) {
+    __shared__ EncLds S;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    // readfirstlane: the wave index is wave-uniform, and the compiler must know it,
+    // or every value merged after the producer/consumer branches becomes a VGPR
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    Blk B;
+    B.in = (gcu8 *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
+    B.dst = (gu8 *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
+    const int nr = a.src_size[b];
+    const int icap = a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride;
+    if (nr < 0 || nr > kMaxBlock || icap < 0) {
+        if (tid == 0) a.result[b] = (nr > kMaxBlock) ? kErange : 0;
+        return;
+    }
+    // withPrefix: the history before the block becomes positions [0, D) of one
+    // 64 KiB window (D a multiple of 64 chunks' worth, so chunk k0 starts the block)
+    int D = 0;
+    if (a.dict_size) {
+        const int pre = a.dict_size[b];
+        D = (pre > 0 ? (pre < kMaxBlock - nr ? pre : kMaxBlock - nr) : 0) & ~63;
+        if (D < 64) D = 0;
+    }
+    B.in -= D;
+    B.n = D + nr;
+    B.nr = (uint32_t)nr;
+    B.k0 = D / 64;
+    // compress_fast's acceleration (:789-808) trades ratio for speed; here that is the
+    // in-chunk candidate (-11 % encode time, ratio -1.7 % on App. C data)
+    B.noL = a.accel > 1;
+    B.cap = (uint32_t)icap;
+    B.un = (uint32_t)B.n;
+    B.mstart = B.un >= 12 ? B.un - 12 : 0;   // matches start at <= n-12 (:585)
+    B.mlimit = B.un >= 5 ? B.un - 5 : 0;     // and end at <= n-5 (:633)
+    B.nch = (B.n + 63) / 64;
+
+    // table = 0 (the reference's memset state: position 0 for every hash)
+    for (int i = tid; i < kHSize / 8; i += 192) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < (int)kScr; i += 192) S.scr[i] = 0xFFFFFFFFu;
+    for (int i = tid; i < (int)(kRingE / 16 + 4); i += 192) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
+    if (tid < 16) S.omap[tid] = 0u;
+    __syncthreads();
+    if (B.n < kSmall) encode_block<true>(S, B, wave, lane, &a.result[b]);
+    else encode_block<false>(S, B, wave, lane, &a.result[b]);
+}
+
+hipError_t launch_encode_v1(const BlockArgs &a, hipStream_t s) {
+    if (a.nblocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lz4_encode_v1_kernel, dim3(a.nblocks), dim3(192), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace apelz4

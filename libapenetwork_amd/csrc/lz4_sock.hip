@@ -1,0 +1,349 @@
+// lz4_sock.hip -- the socket path of the batched codec, host side (BASELINE config 5,
+// SURVEY.md 8(f) rows 1-2): ape_buffer's growable receive buffer made pinned, the
+// receiver's frame parser rewritten, and TX / RX loops that move framed independent
+// blocks between host memory, a socket and the GPU kernels.
+//
+// Reference: the socket receives into `buffer` (malloc/realloc, src/ape_buffer.c:210-228)
+// and parses [int32 size][LZ4 block] frames in ape_socket_read_lz4_stream
+// (src/ape_socket.c:1333-1467).  That parser desyncs: it copies header bytes
+// to `&current_block_size + decompress_position` -- uint32 pointer arithmetic, so a header
+// split across reads lands 4 bytes per byte apart (:1372-1374) -- advances
+// `decompress_position` by the whole read instead of the header bytes taken (:1379), and
+// memmoves from an already-advanced pointer (:1459).  Here:
+//   * APE_LZ4_rxbuf is the `buffer` analogue: APE_LZ4_rxbuf_prepare(b, n) guarantees n
+//     free bytes like buffer_prepare (realloc), and re-registers the storage with
+//     hipHostRegister, so the frames are DMA'd to the GPU straight from it;
+//   * APE_LZ4_rxbuf_frames parses only from a buffer that holds everything received and
+//     not yet consumed, header and block bytes alike, so a header or block split over
+//     any number of reads is just "not complete yet"; sizes are validated before use;
+//   * APE_LZ4_socket_send_blocks / _recv_blocks run the whole path on one connection:
+//     TX = H2D blocks -> encode -> frame offsets + pack -> D2H -> write(); RX = read()
+//     into the pinned rxbuf -> parse -> H2D frames -> decode from frames -> D2H blocks.
+//     Each side double-buffers, so socket I/O of one batch overlaps the GPU work of the
+//     next.  The event loop is not rebuilt: these are blocking calls for one connection
+//     (a caller runs TX and RX on their own threads, as the loopback benchmark does).
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "../../include/ape_lz4_gpu.h"
+#include "lz4_gpu_internal.h"
+
+using namespace apelz4;
+
+struct APE_LZ4_rxbuf {
+    char *data;
+    size_t size, used;
+    int registered;
+};
+
+namespace {
+
+inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
+inline int bound_of(int n) { return n + n / 255 + 16; }
+
+void rx_unregister(APE_LZ4_rxbuf *b) {
+    if (b->registered) (void)hipHostUnregister(b->data);
+    b->registered = 0;
+}
+
+int rx_register(APE_LZ4_rxbuf *b) {
+    if (!b->data || b->registered) return 0;
+    if (hipHostRegister(b->data, b->size, hipHostRegisterDefault) != hipSuccess) return -1;
+    b->registered = 1;
+    return 0;
+}
+
+// write all of buf to fd (blocking), retrying on EINTR / short writes
+long long write_all(int fd, const char *buf, size_t len) {
+    size_t done = 0;
+    while (done < len) {
+        const ssize_t w = write(fd, buf + done, len - done);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return -1;
+        }
+        done += (size_t)w;
+    }
+    return (long long)done;
+}
+
+struct Dev {   // device buffers of one batch slot
+    char *src = nullptr, *comp = nullptr, *frames = nullptr, *out = nullptr;
+    int *csz = nullptr, *sizes = nullptr, *res = nullptr;
+    long long *off = nullptr;
+    void *scratch = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t ev = nullptr;
+};
+
+int dev_alloc(Dev &d, int batch, int bs, bool tx) {
+    const size_t slot = up16((size_t)bound_of(bs));
+    bool ok = hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&d.ev, hipEventDisableTiming) == hipSuccess &&
+              hipMalloc((void **)&d.frames, (size_t)batch * (slot + 4) + 64) == hipSuccess &&
+              hipMalloc((void **)&d.off, ((size_t)batch + 1) * sizeof(long long)) == hipSuccess &&
+              hipMalloc((void **)&d.sizes, (size_t)batch * sizeof(int)) == hipSuccess;
+    if (ok && tx)
+        ok = hipMalloc((void **)&d.src, (size_t)batch * bs) == hipSuccess &&
+             hipMalloc((void **)&d.comp, (size_t)batch * slot) == hipSuccess &&
+             hipMalloc((void **)&d.csz, (size_t)batch * sizeof(int)) == hipSuccess &&
+             hipMalloc(&d.scratch, APE_LZ4_frame_scratch_size(batch) + 16) == hipSuccess;
+    if (ok && !tx)
+        ok = hipMalloc((void **)&d.out, (size_t)batch * bs) == hipSuccess &&
+             hipMalloc((void **)&d.res, (size_t)batch * sizeof(int)) == hipSuccess;
+    if (ok) {
+        int *h = (int *)malloc((size_t)batch * sizeof(int));
+        ok = h != nullptr;
+        if (ok) {
+            for (int i = 0; i < batch; i++) h[i] = bs;
+            ok = hipMemcpy(d.sizes, h, (size_t)batch * sizeof(int), hipMemcpyHostToDevice) == hipSuccess;
+            free(h);
+        }
+    }
+    return ok ? 0 : -1;
+}
+
+void dev_free(Dev &d) {
+    if (d.st) (void)hipStreamSynchronize(d.st);
+    for (void *p : {(void *)d.src, (void *)d.comp, (void *)d.frames, (void *)d.out, (void *)d.csz,
+                    (void *)d.sizes, (void *)d.res, (void *)d.off, d.scratch})
+        if (p) (void)hipFree(p);
+    if (d.ev) (void)hipEventDestroy(d.ev);
+    if (d.st) (void)hipStreamDestroy(d.st);
+    d = Dev();
+}
+
+}  // namespace
+
+extern "C" {
+
+APE_LZ4_rxbuf *APE_LZ4_rxbuf_new(size_t initial) {
+    APE_LZ4_rxbuf *b = (APE_LZ4_rxbuf *)calloc(1, sizeof *b);
+    if (!b) return nullptr;
+    if (initial && APE_LZ4_rxbuf_prepare(b, initial) != 0) {
+        free(b);
+        return nullptr;
+    }
+    return b;
+}
+
+// buffer_prepare (ref src/ape_buffer.c:210-228): at least `more` free bytes after `used`;
+// growth doubles the storage (realloc) and re-registers it for DMA.
+int APE_LZ4_rxbuf_prepare(APE_LZ4_rxbuf *b, size_t more) {
+    if (!b) return -1;
+    if (b->size - b->used >= more && b->data) return 0;
+    size_t ns = b->size ? b->size : 4096;
+    while (ns - b->used < more) ns *= 2;
+    rx_unregister(b);
+    char *p = (char *)realloc(b->data, ns);
+    if (!p) {
+        (void)rx_register(b);
+        return -1;
+    }
+    b->data = p;
+    b->size = ns;
+    (void)rx_register(b);   // without a device the storage stays pageable (still correct)
+    return 0;
+}
+
+char *APE_LZ4_rxbuf_data(APE_LZ4_rxbuf *b) { return b ? b->data : nullptr; }
+size_t APE_LZ4_rxbuf_used(const APE_LZ4_rxbuf *b) { return b ? b->used : 0; }
+size_t APE_LZ4_rxbuf_room(const APE_LZ4_rxbuf *b) { return b ? b->size - b->used : 0; }
+int APE_LZ4_rxbuf_pinned(const APE_LZ4_rxbuf *b) { return b ? b->registered : 0; }
+
+// append raw bytes (what a read() into the buffer does); returns 0 or -1
+int APE_LZ4_rxbuf_append(APE_LZ4_rxbuf *b, const char *data, size_t len) {
+    if (APE_LZ4_rxbuf_prepare(b, len) != 0) return -1;
+    memcpy(b->data + b->used, data, len);
+    b->used += len;
+    return 0;
+}
+
+// Complete frames [le32 size][block] at the start of the buffer: off[i] = frame i's
+// header position (i < n), off[n] = the end of the last complete frame.  At most
+// max_frames; a size < 0 or > max_block is malformed: -1 (the stream is unusable, as
+// the reference socket's decode error, src/ape_socket.c:1393-1396).
+int APE_LZ4_rxbuf_frames(const APE_LZ4_rxbuf *b, long long *off, int max_frames, int max_block) {
+    if (!b || !off || max_frames < 0) return -1;
+    size_t pos = 0;
+    int n = 0;
+    while (n < max_frames && b->used - pos >= 4) {
+        const unsigned char *h = (const unsigned char *)b->data + pos;
+        const uint32_t sz = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) |
+                            ((uint32_t)h[3] << 24);
+        if ((int32_t)sz < 0 || (int32_t)sz > max_block) return -1;
+        if (b->used - pos - 4 < sz) break;   // the block is not all here yet
+        off[n++] = (long long)pos;
+        pos += 4 + (size_t)sz;
+    }
+    off[n] = (long long)pos;
+    return n;
+}
+
+// drop the first n bytes (consumed frames), keeping the rest at the start
+void APE_LZ4_rxbuf_consume(APE_LZ4_rxbuf *b, size_t n) {
+    if (!b) return;
+    if (n >= b->used) {
+        b->used = 0;
+        return;
+    }
+    memmove(b->data, b->data + n, b->used - n);
+    b->used -= n;
+}
+
+void APE_LZ4_rxbuf_free(APE_LZ4_rxbuf *b) {
+    if (!b) return;
+    rx_unregister(b);
+    free(b->data);
+    free(b);
+}
+
+// TX: compress nblocks blocks of block_size bytes (block i at h_src + i*src_stride) on the
+// current device, `batch` at a time, and write the framed stream to fd.  Returns the
+// bytes written, or a negative APE_LZ4_GPU_E* code.
+long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_stride,
+                                     int block_size, int nblocks, int batch) {
+    if (fd < 0 || !h_src || block_size <= 0 || block_size > kMaxBlock || nblocks < 0 || batch <= 0 ||
+        src_stride < (size_t)block_size)
+        return APE_LZ4_GPU_EINVAL;
+    int rc = APE_LZ4_gpu_init();
+    if (rc) return rc;
+    const size_t slot = up16((size_t)bound_of(block_size));
+    Dev d[2];
+    char *hf[2] = {nullptr, nullptr};
+    long long *htot[2] = {nullptr, nullptr};
+    long long sent = 0;
+    int nb[2] = {0, 0};
+    const int nbat = (nblocks + batch - 1) / batch;
+    for (int i = 0; i < 2 && rc == 0; i++) {
+        if (dev_alloc(d[i], batch, block_size, true) != 0 ||
+            hipHostMalloc((void **)&hf[i], (size_t)batch * (slot + 4) + 64, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void **)&htot[i], sizeof(long long), hipHostMallocDefault) != hipSuccess)
+            rc = APE_LZ4_GPU_ENOMEM;
+    }
+    auto launch = [&](int c) -> int {
+        Dev &D = d[c & 1];
+        const int k = nblocks - c * batch < batch ? nblocks - c * batch : batch;
+        nb[c & 1] = k;
+        const char *src = h_src + (size_t)c * batch * src_stride;
+        hipError_t e = hipMemcpy2DAsync(D.src, (size_t)block_size, src, src_stride, (size_t)block_size,
+                                        (size_t)k, hipMemcpyHostToDevice, D.st);
+        if (e != hipSuccess) return APE_LZ4_GPU_ELAUNCH;
+        int r = APE_LZ4_compress_batch_strided_dev(D.src, (size_t)block_size, D.sizes, D.comp, slot,
+                                                   nullptr, D.csz, k, D.st);
+        if (r == 0) r = APE_LZ4_frame_offsets_dev(D.csz, D.off, D.scratch, k, D.st);
+        if (r == 0) r = APE_LZ4_frame_pack_strided_dev(D.comp, slot, D.csz, D.off, D.frames, k, D.st);
+        if (r) return r;
+        e = hipMemcpyAsync(htot[c & 1], D.off + k, sizeof(long long), hipMemcpyDeviceToHost, D.st);
+        if (e == hipSuccess) e = hipEventRecord(D.ev, D.st);
+        return e == hipSuccess ? 0 : APE_LZ4_GPU_ELAUNCH;
+    };
+    if (rc == 0 && nbat > 0) rc = launch(0);
+    for (int c = 0; c < nbat && rc == 0; c++) {
+        Dev &D = d[c & 1];
+        if (hipEventSynchronize(D.ev) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        const long long tot = *htot[c & 1];
+        if (hipMemcpyAsync(hf[c & 1], D.frames, (size_t)tot, hipMemcpyDeviceToHost, D.st) != hipSuccess ||
+            hipStreamSynchronize(D.st) != hipSuccess) {
+            rc = APE_LZ4_GPU_ELAUNCH;
+            break;
+        }
+        if (c + 1 < nbat) rc = launch(c + 1);   // the next batch's GPU work under this write
+        if (rc) break;
+        const long long w = write_all(fd, hf[c & 1], (size_t)tot);
+        if (w < 0) { rc = APE_LZ4_GPU_EINVAL; break; }
+        sent += w;
+    }
+    for (int i = 0; i < 2; i++) {
+        dev_free(d[i]);
+        if (hf[i]) (void)hipHostFree(hf[i]);
+        if (htot[i]) (void)hipHostFree(htot[i]);
+    }
+    return rc ? rc : sent;
+}
+
+// RX: read the framed stream from fd into pinned rxbufs, decode `batch` frames at a time
+// on the current device into block i at h_dst + i*dst_stride (capacity block_size),
+// h_result[i] = decompress_safe's result.  Returns the blocks received, or a negative
+// APE_LZ4_GPU_E* code (APE_LZ4_GPU_EINVAL also for a malformed frame or early EOF).
+long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int block_size,
+                                     int nblocks, int batch, int *h_result) {
+    if (fd < 0 || !h_dst || !h_result || block_size <= 0 || nblocks < 0 || batch <= 0 ||
+        dst_stride < (size_t)block_size)
+        return APE_LZ4_GPU_EINVAL;
+    int rc = APE_LZ4_gpu_init();
+    if (rc) return rc;
+    const int maxc = bound_of(block_size);
+    const size_t chunk = 1u << 20;   // read() granularity
+    Dev d[2];
+    APE_LZ4_rxbuf *rb[2] = {APE_LZ4_rxbuf_new(4u << 20), APE_LZ4_rxbuf_new(4u << 20)};
+    long long *hoff[2] = {nullptr, nullptr};
+    bool busy[2] = {false, false};
+    for (int i = 0; i < 2 && rc == 0; i++) {
+        if (!rb[i] || dev_alloc(d[i], batch, block_size, false) != 0 ||
+            hipHostMalloc((void **)&hoff[i], ((size_t)batch + 1) * sizeof(long long),
+                          hipHostMallocDefault) != hipSuccess)
+            rc = APE_LZ4_GPU_ENOMEM;
+    }
+    long long done = 0;       // blocks handed to the GPU
+    int cur = 0;              // rxbuf receiving
+    bool eof = false;
+    while (rc == 0 && done < nblocks) {
+        APE_LZ4_rxbuf *b = rb[cur];
+        const int want = nblocks - done < batch ? (int)(nblocks - done) : batch;
+        const int n = APE_LZ4_rxbuf_frames(b, hoff[cur], want, maxc);
+        if (n < 0) { rc = APE_LZ4_GPU_EINVAL; break; }
+        if (n < want) {   // read more
+            if (eof) { rc = APE_LZ4_GPU_EINVAL; break; }
+            if (APE_LZ4_rxbuf_prepare(b, chunk) != 0) { rc = APE_LZ4_GPU_ENOMEM; break; }
+            const ssize_t r = read(fd, b->data + b->used, b->size - b->used);
+            if (r < 0) {
+                if (errno == EINTR) continue;
+                rc = APE_LZ4_GPU_EINVAL;
+                break;
+            }
+            if (r == 0) eof = true;
+            b->used += (size_t)r;
+            continue;
+        }
+        // a full batch: hand this buffer to the GPU, continue receiving in the other one
+        const int nxt = cur ^ 1;
+        if (busy[nxt]) {
+            if (hipStreamSynchronize(d[nxt].st) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+            busy[nxt] = false;
+        }
+        const size_t end = (size_t)hoff[cur][n];
+        APE_LZ4_rxbuf *o = rb[nxt];
+        o->used = 0;
+        if (APE_LZ4_rxbuf_append(o, b->data + end, b->used - end) != 0) { rc = APE_LZ4_GPU_ENOMEM; break; }
+        b->used = end;
+        Dev &D = d[cur];
+        hipError_t e = hipMemcpyAsync(D.frames, b->data, end, hipMemcpyHostToDevice, D.st);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(D.off, hoff[cur], ((size_t)n + 1) * sizeof(long long),
+                               hipMemcpyHostToDevice, D.st);
+        if (e != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        rc = APE_LZ4_decompress_safe_frames_dev(D.frames, D.off, D.out, (size_t)block_size, D.sizes,
+                                                D.res, n, D.st);
+        if (rc) break;
+        e = hipMemcpy2DAsync(h_dst + (size_t)done * dst_stride, dst_stride, D.out, (size_t)block_size,
+                             (size_t)block_size, (size_t)n, hipMemcpyDeviceToHost, D.st);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(h_result + done, D.res, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, D.st);
+        if (e != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        busy[cur] = true;
+        done += n;
+        cur = nxt;
+    }
+    for (int i = 0; i < 2; i++) {
+        dev_free(d[i]);
+        APE_LZ4_rxbuf_free(rb[i]);
+        if (hoff[i]) (void)hipHostFree(hoff[i]);
+    }
+    return rc ? rc : done;
+}
+
+}  // extern "C"

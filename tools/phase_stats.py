@@ -16,8 +16,9 @@ sys.path.insert(0, ROOT)
 DEC = ["parse", "copy", "(batches)", "(steps)", "(restages)", "(division steps)",
        "(in-step source steps)", "(resolution passes)", "(HBM-read steps)", "", "(blocks)", "", "",
        "", "", ""]
-ENC = ["W walk", "W publish", "E write", "W wait end", "W wait mid", "P A+B+C1",
-       "P wait mid", "P C2", "P wait end", "", "(steps x3 waves)", "(members)", "E prepare",
+ENC = ["W walk", "W publish", "E load", "W wait end", "W wait mid", "P F+M+H+L",
+       "P wait mid", "P wait end", "(sequences)", "(batches)", "(steps x3 waves)",
+       "(walker extensions)", "E store",
        "(blocks)", "E wait mid", "E wait end"]
 
 
