@@ -17,6 +17,8 @@ oracle = the reference decoder restated) and the compression ratio is reported.
 
 Also in the line (rank 0, N = 1): `config2` = BASELINE config 2 (256K x 4 KiB random blocks
 compressed by the reference algorithm, decode only) with its own roofline and CPU baseline;
+`config5` = BASELINE config 5 through a real byte path: GPU encode -> frames -> one loopback
+TCP connection -> pinned growable rxbuf + frame parser -> GPU decode (sock_leg, 1 GiB);
 `cpu_baseline` = the reference src/ape_lz4.c built from its own source with gcc and clang
 (oracle/_ref), a 1..N thread sweep over the box's usable cores on a 4 GiB sample;
 `roofline` = the dominant kernel's algorithmic bytes / its HIP-event time, plus the
@@ -503,6 +505,94 @@ def stream_bench(args):
     print(json.dumps(line), flush=True)
 
 
+def sock_leg(args):
+    """BASELINE config 5 through a real byte path: a loopback TCP connection.
+
+    TX thread: APE_LZ4_socket_send_blocks -- host blocks --H2D--> encode --> frames
+    --D2H--> write().  RX (this thread): APE_LZ4_socket_recv_blocks -- read() into the
+    pinned growable rxbuf (the ape_buffer analogue) --> frame parser (K7 rewritten) --H2D-->
+    decode from the frames --D2H--> host blocks.  Both sides double-buffer, so the socket
+    I/O of one batch overlaps the GPU work of the next.  Rate = uncompressed bytes / wall
+    time from the first send to the last received block; every block is compared."""
+    import socket
+    import threading
+
+    import torch
+
+    import libapenetwork_amd as amd
+
+    torch.cuda.set_device(0)
+    if amd.gpu_init() != 0:
+        raise SystemExit("GPU codec unavailable: %s" % amd.gpu_last_error())
+    n, nb, batch = args.block_size, args.sock_blocks, args.sock_batch
+    kind = 1 if args.kind == "comp" else 0
+    h_src = torch.empty((nb, n), dtype=torch.uint8, pin_memory=True)
+    h_dst = torch.zeros((nb, n), dtype=torch.uint8, pin_memory=True)
+    res = np.zeros(nb, dtype=np.int32)
+    g = torch.empty((min(nb, 8192), n), dtype=torch.uint8, device="cuda")
+    for lo in range(0, nb, g.shape[0]):
+        k = min(g.shape[0], nb - lo)
+        amd.synth_blocks(g[:k], n, lo, kind)
+        h_src[lo:lo + k].copy_(g[:k])
+    torch.cuda.synchronize()
+    del g
+    src_np, dst_np = h_src.numpy(), h_dst.numpy()
+
+    def run(k):
+        srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        srv.bind(("127.0.0.1", 0))
+        srv.listen(1)
+        tx = socket.create_connection(srv.getsockname())
+        rx, _ = srv.accept()
+        srv.close()
+        for s_ in (tx, rx):
+            s_.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
+            s_.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
+        sent = {}
+
+        def txf():
+            try:
+                sent["bytes"] = amd.socket_send_blocks(tx.fileno(), src_np[:k], n, batch)
+            except Exception as e:   # reported below
+                sent["err"] = e
+            finally:
+                tx.shutdown(socket.SHUT_WR)
+
+        t0 = time.perf_counter()
+        th = threading.Thread(target=txf)
+        th.start()
+        got = amd.socket_recv_blocks(rx.fileno(), dst_np[:k], n, batch, res[:k])
+        th.join()
+        wall = time.perf_counter() - t0
+        tx.close()
+        rx.close()
+        if "err" in sent:
+            raise sent["err"]
+        return wall, got, sent["bytes"]
+
+    run(min(nb, 2 * batch))                    # warm-up (kernels, allocations)
+    h_dst.zero_()
+    wall, got, wire = run(nb)
+    ok = got == nb and bool((res == n).all()) and bool(torch.equal(h_dst, h_src))
+    return {
+        "metric": "LZ4 GiB/s through a loopback TCP socket (GPU encode -> frames -> socket -> "
+                  "pinned rxbuf -> GPU decode), BASELINE config 5",
+        "value": round(nb * n / wall / GIB, 3), "unit": "GiB/s", "n_gpus": 1,
+        "higher_is_better": True, "dtype": "u8",
+        "data": "synthetic (SURVEY App. C gen_%s)" % args.kind,
+        "config": {"workload": "%d x %d KiB blocks over one 127.0.0.1 TCP connection, %d blocks "
+                               "per GPU batch" % (nb, n >> 10, batch)},
+        "wall_s": round(wall, 3), "wire_bytes": int(wire), "ratio": round(nb * n / (wire - 4 * nb), 4),
+        "wire_GBps": round(wire / wall / 1e9, 3), "verified": ok,
+        "reference_loopback_GiBps": "0.25-0.33 (BASELINE.md config 5, reference CPU codec)",
+    }
+
+
+def sock_bench(args):
+    print(json.dumps(sock_leg(args)), flush=True)
+
+
 def sq_issue(kernel):
     """Instruction-issue occupancy of `kernel` from the committed SQ PMC passes
     (profiles/sq_issue.json, PROFILE-DERIVED): the binding resource of this integer
@@ -598,6 +688,7 @@ def main():
                     help="CPU-baseline sample (65536 x 64 KiB = 4 GiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config2", action="store_true")
+    ap.add_argument("--no-config5", action="store_true")
     ap.add_argument("--config2-blocks", type=int, default=1 << 18)
     ap.add_argument("--verify-sample", type=int, default=64)
     ap.add_argument("--e2e", action="store_true",
@@ -612,9 +703,15 @@ def main():
     ap.add_argument("--stream-blocks", type=int, default=1 << 17)
     ap.add_argument("--stream-chunk", type=int, default=8192)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--sock", action="store_true",
+                    help="config 5: loopback TCP socket TX/RX through the GPU codec")
+    ap.add_argument("--sock-blocks", type=int, default=1 << 14)
+    ap.add_argument("--sock-batch", type=int, default=2048)
     args = ap.parse_args()
     if args.e2e:
         return e2e_bench(args)
+    if args.sock:
+        return sock_bench(args)
     if args.stream:
         return stream_bench(args)
     if args.rand4k:
@@ -773,6 +870,14 @@ def main():
         if not args.no_cpu_baseline:
             c2["cpu_baseline"] = cpu_baseline(4096, 0, args.config2_blocks, mode=1)
 
+    c5 = None
+    if rank == 0 and world == 1 and not args.no_config5:
+        try:
+            torch.cuda.empty_cache()
+            c5 = sock_leg(args)
+        except Exception as e:   # the socket leg never masks the headline line
+            c5 = {"error": repr(e)}
+
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
@@ -793,7 +898,7 @@ def main():
                                   "frac": round(value / read_bound, 4)},
             "per_gpu": per_rank,
             "verified": bool(ok), "oracle_sample_ok": sample_ok,
-            "roofline": roof, "cpu_baseline": cpu, "config2": c2,
+            "roofline": roof, "cpu_baseline": cpu, "config2": c2, "config5": c5,
         }
         print(json.dumps(line), flush=True)
     if dist:

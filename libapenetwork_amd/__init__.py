@@ -18,7 +18,8 @@ __all__ = [
     "decompress_partial_batch", "synth_blocks", "gpu_init", "gpu_last_error", "GpuError",
     "MAX_BLOCK", "ERANGE", "frame_offsets", "frame_pack", "decompress_frames",
     "compress_prefix_batch", "decompress_dict_batch", "compress_fast_ptr_batch",
-    "decompress_fast_ptr_batch", "compress_destSize_ptr_batch",
+    "decompress_fast_ptr_batch", "compress_destSize_ptr_batch", "RxBuf",
+    "socket_send_blocks", "socket_recv_blocks",
 ]
 
 _HERE = _os.path.dirname(_os.path.abspath(__file__))
@@ -69,6 +70,18 @@ def lib():
             "APE_LZ4_decompress_safe_frames_dev": (i, [p, p, p, sz, p, p, i, p]),
             "APE_LZ4_compress_withPrefix_batch_dev": (i, [p, p, p, p, p, p, i, p]),
             "APE_LZ4_decompress_safe_usingDict_batch_dev": (i, [p, p, p, p, p, p, p, i, p]),
+            "APE_LZ4_rxbuf_new": (p, [sz]),
+            "APE_LZ4_rxbuf_prepare": (i, [p, sz]),
+            "APE_LZ4_rxbuf_append": (i, [p, p, sz]),
+            "APE_LZ4_rxbuf_frames": (i, [p, p, i, i]),
+            "APE_LZ4_rxbuf_consume": (None, [p, sz]),
+            "APE_LZ4_rxbuf_data": (p, [p]),
+            "APE_LZ4_rxbuf_used": (sz, [p]),
+            "APE_LZ4_rxbuf_room": (sz, [p]),
+            "APE_LZ4_rxbuf_pinned": (i, [p]),
+            "APE_LZ4_rxbuf_free": (None, [p]),
+            "APE_LZ4_socket_send_blocks": (ll, [i, p, sz, i, i, i]),
+            "APE_LZ4_socket_recv_blocks": (ll, [i, p, sz, i, i, i, p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -263,3 +276,77 @@ def decompress_frames(frames, offsets, dst, results, dst_caps=None, nblocks=None
                                                     dst.stride(0), _ptr(dst_caps), _ptr(results),
                                                     n, _stream(stream)),
            "APE_LZ4_decompress_safe_frames_dev")
+
+
+# ---- socket path (include/ape_lz4_gpu.h, lz4_sock.hip; BASELINE config 5) ----
+class RxBuf:
+    """APE_LZ4_rxbuf: the receive buffer of ape_socket (ref src/ape_buffer.c:210-228),
+    growable and registered for DMA, with the rewritten frame parser."""
+
+    def __init__(self, initial=0):
+        self._b = lib().APE_LZ4_rxbuf_new(initial)
+        if not self._b:
+            raise MemoryError("APE_LZ4_rxbuf_new")
+
+    def prepare(self, more):
+        return lib().APE_LZ4_rxbuf_prepare(self._b, more)
+
+    def append(self, data):
+        data = bytes(data)
+        return lib().APE_LZ4_rxbuf_append(self._b, data, len(data))
+
+    def frames(self, max_frames, max_block):
+        """(n, offsets[0..n]) of the complete frames at the start, or (-1, []) if malformed."""
+        off = (_C.c_longlong * (max_frames + 1))()
+        n = lib().APE_LZ4_rxbuf_frames(self._b, off, max_frames, max_block)
+        return n, (list(off[:n + 1]) if n >= 0 else [])
+
+    def consume(self, n):
+        lib().APE_LZ4_rxbuf_consume(self._b, n)
+
+    def used(self):
+        return lib().APE_LZ4_rxbuf_used(self._b)
+
+    def room(self):
+        return lib().APE_LZ4_rxbuf_room(self._b)
+
+    def pinned(self):
+        return bool(lib().APE_LZ4_rxbuf_pinned(self._b))
+
+    def data(self):
+        n = self.used()
+        return _C.string_at(lib().APE_LZ4_rxbuf_data(self._b), n) if n else b""
+
+    def free(self):
+        if self._b:
+            lib().APE_LZ4_rxbuf_free(self._b)
+            self._b = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def socket_send_blocks(fd, src, block_size, batch):
+    """APE_LZ4_socket_send_blocks: rows of src (uint8 numpy [N, S] or CPU tensor, S >=
+    block_size) -> GPU encode -> framed stream written to fd.  Returns bytes written."""
+    n = int(src.shape[0])
+    stride = int(src.strides[0]) if hasattr(src, "strides") else int(src.stride(0))
+    ptr = src.ctypes.data if hasattr(src, "ctypes") else src.data_ptr()
+    r = lib().APE_LZ4_socket_send_blocks(fd, _C.c_void_p(ptr), stride, block_size, n, batch)
+    if r < 0:
+        raise GpuError("APE_LZ4_socket_send_blocks failed (%d): %s" % (r, gpu_last_error()))
+    return r
+
+
+def socket_recv_blocks(fd, dst, block_size, batch, results):
+    """APE_LZ4_socket_recv_blocks: framed stream read from fd -> GPU decode -> rows of dst
+    (uint8 numpy [N, S]); results (int32 numpy [N]) = decompress_safe results."""
+    n = int(dst.shape[0])
+    r = lib().APE_LZ4_socket_recv_blocks(fd, _C.c_void_p(dst.ctypes.data), int(dst.strides[0]),
+                                         block_size, n, batch, _C.c_void_p(results.ctypes.data))
+    if r < 0:
+        raise GpuError("APE_LZ4_socket_recv_blocks failed (%d): %s" % (r, gpu_last_error()))
+    return r

@@ -401,7 +401,10 @@ __device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t bas
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             // one nontemporal byte load for both sources (history in dst must bypass
-            // this CU's L1; the literal in src does not care); idle lanes read src[0]
+            // this CU's L1; the literal in src does not care); idle lanes read src[0].
+            // A/B (tools/dec_variants.sh, 65536 blocks): device-scope loads that allocate
+            // in L2 fetch as much (the history misses L2 either way: ~1000 blocks per XCD
+            // stream their output through its 4 MB) and take 12% longer.
             gcu8 *bp = gk[j] == 2u ? (gcu8 *)D.dst : D.src;
             const uint32_t o = gk[j] != 0u ? pos[j] : 0u;
             if (DICT && gk[j] == 3u) bp = D.dend - 0x100000000ll;   // dend + (int32)o

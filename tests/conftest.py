@@ -6,6 +6,14 @@ import sys
 
 import pytest
 
+# torch first: its wheel carries its own HIP runtime, and loading /opt/rocm's (through
+# libape_lz4_amd.so) before it leaves torch.cuda unavailable in that process (the
+# library works either way).  Plumbing only: no test needs torch on CPU.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 sys.path.insert(0, ROOT)

@@ -1,0 +1,222 @@
+"""Socket path (BASELINE config 5; lz4_sock.hip): the receive buffer and its frame parser
+(the rewrite of ape_socket_read_lz4_stream, ref src/ape_socket.c:1333-1467, whose header
+handling desyncs -- SURVEY K7: :1372-1374 uint32 pointer arithmetic, :1379 position
+advanced by the whole read, :1459 memmove from an advanced pointer), and the loopback TCP
+TX/RX through the GPU codec.
+
+CPU tests: frames split at every possible point (1-byte reads, headers split over
+reads, several frames per read) are recovered exactly; malformed sizes are rejected
+(ref :1382-1384 bounds the size by APE_LZ4_BLOCK_COMP_SIZE).  GPU tests: a real
+127.0.0.1 connection, blocks compared byte for byte, the host output pads untouched."""
+import random
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+
+def frame(blocks):
+    out = bytearray()
+    for b in blocks:
+        out += len(b).to_bytes(4, "little") + b
+    return bytes(out)
+
+
+def feed_and_parse(product, stream, cuts, max_block, max_frames=1000):
+    """Append `stream` in pieces at `cuts`; after each append take the complete frames."""
+    rb = product.RxBuf(0)
+    got = []
+    prev = 0
+    for c in list(cuts) + [len(stream)]:
+        assert rb.append(stream[prev:c]) == 0
+        prev = c
+        n, off = rb.frames(max_frames, max_block)
+        assert n >= 0
+        data = rb.data()
+        for i in range(n):
+            sz = int.from_bytes(data[off[i]:off[i] + 4], "little")
+            assert off[i + 1] == off[i] + 4 + sz
+            got.append(data[off[i] + 4:off[i + 1]])
+        rb.consume(off[n])
+    assert rb.used() == 0
+    rb.free()
+    return got
+
+
+def test_rxbuf_every_split_point(product):
+    rng = random.Random(5)
+    blocks = [bytes(rng.getrandbits(8) for _ in range(k)) for k in (0, 1, 3, 4, 5, 17, 300)]
+    stream = frame(blocks)
+    for c in range(len(stream) + 1):   # one cut anywhere, headers included
+        assert feed_and_parse(product, stream, [c], 1000) == blocks
+
+
+def test_rxbuf_one_byte_reads_and_random_reads(product):
+    rng = random.Random(7)
+    blocks = [bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 2000))) for _ in range(60)]
+    stream = frame(blocks)
+    assert feed_and_parse(product, stream, range(1, len(stream)), 4096) == blocks
+    for _ in range(20):
+        cuts = sorted(rng.sample(range(1, len(stream)), rng.randrange(1, 200)))
+        assert feed_and_parse(product, stream, cuts, 4096) == blocks
+
+
+def test_rxbuf_max_frames_and_partial(product):
+    blocks = [b"a" * 10, b"b" * 20, b"c" * 30]
+    stream = frame(blocks)
+    rb = product.RxBuf(16)
+    rb.append(stream[:-1])                    # the last block is one byte short
+    n, off = rb.frames(1, 100)
+    assert n == 1 and off == [0, 14]
+    n, off = rb.frames(10, 100)
+    assert n == 2 and off == [0, 14, 38]
+    rb.append(stream[-1:])
+    n, off = rb.frames(10, 100)
+    assert n == 3 and off[-1] == len(stream)
+    rb.free()
+
+
+@pytest.mark.parametrize("size", [-1, -2147483648, 101, 0x7FFFFFFF])
+def test_rxbuf_malformed_size(product, size):
+    rb = product.RxBuf(0)
+    rb.append(frame([b"ok"]) + (size & 0xFFFFFFFF).to_bytes(4, "little") + b"x" * 8)
+    n, off = rb.frames(10, 100)
+    assert n == -1 and off == []
+    rb.free()
+
+
+def test_rxbuf_growth_keeps_bytes(product):
+    rb = product.RxBuf(0)
+    assert rb.used() == 0
+    rng = random.Random(9)
+    data = bytes(rng.getrandbits(8) for _ in range(100000))
+    for k in range(0, len(data), 7919):
+        assert rb.append(data[k:k + 7919]) == 0
+    assert rb.used() == len(data) and rb.data() == data
+    assert rb.prepare(1 << 20) == 0 and rb.room() >= 1 << 20
+    assert rb.data() == data
+    rb.consume(12345)
+    assert rb.data() == data[12345:]
+    rb.free()
+
+
+# ---------------- GPU: loopback TCP through the codec ----------------
+def _pair():
+    srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    tx = socket.create_connection(srv.getsockname())
+    rx, _ = srv.accept()
+    srv.close()
+    return tx, rx
+
+
+def _blocks(cuda, product, nb, n, kind):
+    g = cuda.empty((nb, n), dtype=cuda.uint8, device="cuda")
+    product.synth_blocks(g, n, 11, kind)
+    return g.cpu().numpy()
+
+
+def _dst(nb, n, pad=64):
+    buf = np.full((nb, n + pad), 0xCB, dtype=np.uint8)
+    return buf
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,batch", [(1, 16), (0, 7), (1, 64)])
+def test_socket_loopback_roundtrip(cuda, product, kind, batch):
+    nb, n = 40, 65536
+    src = _blocks(cuda, product, nb, n, kind)
+    dst = _dst(nb, n)
+    res = np.zeros(nb, dtype=np.int32)
+    tx, rx = _pair()
+    out = {}
+
+    def txf():
+        out["sent"] = product.socket_send_blocks(tx.fileno(), src, n, batch)
+        tx.shutdown(socket.SHUT_WR)
+
+    th = threading.Thread(target=txf)
+    th.start()
+    got = product.socket_recv_blocks(rx.fileno(), dst, n, batch, res)
+    th.join()
+    tx.close()
+    rx.close()
+    assert got == nb
+    assert (res == n).all()
+    assert np.array_equal(dst[:, :n], src)
+    assert (dst[:, n:] == 0xCB).all()            # nothing past each block's capacity
+    assert out["sent"] > 4 * nb
+
+
+def _gpu_frames(cuda, product, src):
+    nb, n = src.shape
+    d = cuda.from_numpy(src).cuda()
+    slot = (product.compressBound(n) + 15) // 16 * 16
+    comp = cuda.empty((nb, slot), dtype=cuda.uint8, device="cuda")
+    csz = cuda.zeros(nb, dtype=cuda.int32, device="cuda")
+    sizes = cuda.full((nb,), n, dtype=cuda.int32, device="cuda")
+    product.compress_batch(d, sizes, comp, csz)
+    off = cuda.zeros(nb + 1, dtype=cuda.int64, device="cuda")
+    product.frame_offsets(csz, off)
+    frames = cuda.empty(nb * (slot + 4), dtype=cuda.uint8, device="cuda")
+    product.frame_pack(comp, csz, off, frames)
+    cuda.cuda.synchronize()
+    return bytes(frames[:int(off[nb].item())].cpu().numpy())
+
+
+def _send_pieces(sock, stream, rng, small_until):
+    """Write the stream in tiny pieces (1-7 bytes: every header split) up to
+    `small_until`, then in random larger pieces."""
+    p = 0
+    while p < len(stream):
+        k = rng.randrange(1, 8) if p < small_until else rng.randrange(1, 70000)
+        sock.sendall(stream[p:p + k])
+        p += k
+    sock.shutdown(socket.SHUT_WR)
+
+
+@pytest.mark.gpu
+def test_socket_recv_fragmented_sender(cuda, product):
+    """K7's trigger: headers split across reads.  A sender writing 1-7 byte pieces."""
+    nb, n = 24, 65536
+    src = _blocks(cuda, product, nb, n, 1)
+    stream = _gpu_frames(cuda, product, src)
+    dst = _dst(nb, n)
+    res = np.zeros(nb, dtype=np.int32)
+    tx, rx = _pair()
+    th = threading.Thread(target=_send_pieces, args=(tx, stream, random.Random(3), 40000))
+    th.start()
+    got = product.socket_recv_blocks(rx.fileno(), dst, n, 5, res)
+    th.join()
+    tx.close()
+    rx.close()
+    assert got == nb and (res == n).all()
+    assert np.array_equal(dst[:, :n], src) and (dst[:, n:] == 0xCB).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("damage", ["truncated", "oversized_header", "negative_header"])
+def test_socket_recv_malformed_stream(cuda, product, damage):
+    nb, n = 6, 65536
+    src = _blocks(cuda, product, nb, n, 1)
+    stream = bytearray(_gpu_frames(cuda, product, src))
+    if damage == "truncated":
+        stream = stream[:-100]
+    else:
+        first = int.from_bytes(stream[0:4], "little")
+        at = 4 + first                            # the second frame's header
+        bad = product.compressBound(n) + 1 if damage == "oversized_header" else 0x80000000
+        stream[at:at + 4] = bad.to_bytes(4, "little")
+    dst = _dst(nb, n)
+    res = np.zeros(nb, dtype=np.int32)
+    tx, rx = _pair()
+    th = threading.Thread(target=lambda: (tx.sendall(bytes(stream)), tx.shutdown(socket.SHUT_WR)))
+    th.start()
+    with pytest.raises(product.GpuError):
+        product.socket_recv_blocks(rx.fileno(), dst, n, 4, res)
+    th.join()
+    tx.close()
+    rx.close()
+    assert (dst[:, n:] == 0xCB).all()

@@ -10,9 +10,9 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_encode.py tests/test_gpu_ap
 rc=$?; tail -4 gpurun_out/pytest_enc.log; echo "pytest rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 B=${1:-131072}
-APE_LZ4_ENCODER=v2 timeout -k 10 200 python -u bench.py --blocks $B --steps 3 --no-cpu-baseline --no-config2 \
+APE_LZ4_ENCODER=v2 timeout -k 10 200 python -u bench.py --blocks $B --steps 3 --no-cpu-baseline --no-config2 --no-config5 \
     > gpurun_out/ab_v2.json 2> gpurun_out/ab_v2.err || exit 1
-timeout -k 10 200 python -u bench.py --blocks $B --steps 3 --no-cpu-baseline \
+timeout -k 10 200 python -u bench.py --blocks $B --steps 3 --no-cpu-baseline --no-config5 \
     --no-config2 > gpurun_out/ab_v1.json 2> gpurun_out/ab_v1.err || exit 1
 python3 - <<'PY'
 import json
