@@ -82,6 +82,9 @@ struct __attribute__((aligned(16))) EncLds {
                                // in lane i: {p | back << 16, len | offset << 16}
     uint32_t qcnt;             // its count (0 = none pending; the emitter resets it)
     uint2 wq[16];              // walker: one chunk's sequences (<= 16: matches are >= 4 long)
+    uint32_t xw[2][40];        // producer: chunk k's bytes in[64k-4, 64k+140) at [k % 2] (from
+                               // L(k) to M(k)): every lane's own window, the in-chunk
+                               // candidate and the stage-2 own segments (36 dwords + pad)
 };
 static_assert(sizeof(EncLds) <= 20480, "8 blocks per CU: 8 x 20 KiB = the 160 KiB LDS");
 
@@ -247,11 +250,50 @@ struct PSet {
     uint32_t lg;                     // stage-2 lanes per candidate, log2 (wave-uniform)
 };
 
-// L(k): own bytes in[p-4, p+12)
+// L(k): the chunk's 144 bytes in[64k-4, 64k+140), one dword per lane 0..35 (bytes
+// outside [0, n) read as 0) -- through the texture path once instead of as 64
+// overlapping 16-byte windows plus the stage-2 own segments; x_spread makes the
+// windows.  Outside SMALL one load instruction.
 template <bool SMALL, bool FAST>
-__device__ __forceinline__ void p_load(const Blk &B, int k, int lane, uint32_t (&X)[4]) {
-    const int pos = (k < B.nch ? 64 * k : 0) + lane - 4;
-    load16<SMALL>(B.in, B.n, pos, X, FAST || (k >= 1 && k < B.nch && 64 * k + 76 <= B.n));
+__device__ __forceinline__ void p_load(const Blk &B, int k, int lane, uint32_t &xd) {
+    // lanes 36..63 repeat lane 35's address (no branch: the compiler's wait-count
+    // model would take a skippable load as not issued and wait for older loads)
+    const int w = (k < B.nch ? 64 * k : 0) - 4 + 4 * (lane < 36 ? lane : 35);
+    if (SMALL) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            if (w + t >= 0 && w + t < B.n) v |= (uint32_t)B.in[(uint32_t)(w + t)] << (8 * t);
+        xd = v;
+    } else if (FAST) {
+        xd = gload4(B.in + (uint32_t)w);
+    } else {   // clamped into [0, n - 4] (n >= 128 here), then shifted into place
+        const int a = w < 0 ? 0 : (w > B.n - 4 ? B.n - 4 : w);
+        const uint32_t v = gload4(B.in + (uint32_t)a);
+        const int d = w - a;   // -4 .. 4
+        const uint32_t dn = d > 0 ? (d < 4 ? v >> (8 * d) : 0u) : 0u;
+        const uint32_t up = d < 0 ? (d > -4 ? v << (-8 * d) : 0u) : 0u;
+        xd = d == 0 ? v : (d > 0 ? dn : up);
+    }
+}
+
+// 16 bytes at byte offset j (0..128) of a chunk image: five dwords, four alignbytes
+__device__ __forceinline__ void x_window(const uint32_t *img, uint32_t j, uint32_t (&X)[4]) {
+    const uint32_t *w = img + (j >> 2);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+    const uint32_t r = j & 3u;
+    X[0] = __builtin_amdgcn_alignbyte(w1, w0, r);
+    X[1] = __builtin_amdgcn_alignbyte(w2, w1, r);
+    X[2] = __builtin_amdgcn_alignbyte(w3, w2, r);
+    X[3] = __builtin_amdgcn_alignbyte(w4, w3, r);
+}
+
+// the loaded dwords of chunk k -> its LDS image -> every lane's own window in[p-4, p+12)
+__device__ __forceinline__ void x_spread(EncLds &S, int k, int lane, uint32_t xd, uint32_t (&X)[4]) {
+    uint32_t *img = S.xw[k & 1];
+    if (lane < 36) img[lane] = xd;
+    wave_sync();
+    x_window(img, (uint32_t)lane, X);
 }
 
 // H(k): hash, table + in-chunk candidates, hash ring, candidate loads
@@ -285,9 +327,9 @@ __device__ __forceinline__ void p_lookup(EncLds &S, const Blk &B, int k, int lan
     C.h = h;
     C.cT = okT ? cT : 0xFFFFFFFFu;
     C.cL = okL ? cL : 0xFFFFFFFFu;
-    // dummy loads of idle lanes read the block start (n >= 16 outside SMALL)
+    // dummy loads of idle lanes read the block start (n >= 16 outside SMALL); the
+    // in-chunk candidate's bytes come from the chunk image in M
     load16<SMALL>(B.in, B.n, okT ? (int)cT - 4 : 0, C.Y, !SMALL);
-    load16<SMALL>(B.in, B.n, okL ? (int)cL - 4 : 0, C.Z, !SMALL);
 }
 
 // first differing byte of A vs B over 4 dwords (0..15), 0x1FFFFFFF if all 16 equal:
@@ -305,6 +347,8 @@ template <bool SMALL, bool FAST>
 __device__ __forceinline__ void p_measure(EncLds &S, const Blk &B, int k, int lane, PSet &C) {
     const uint32_t (&X)[4] = C.X;
     const PSet &Sh = C;
+    // in-chunk candidate bytes [cL-4, cL+12) = image bytes [cL - 64k, +16)
+    x_window(S.xw[k & 1], C.cL != 0xFFFFFFFFu ? C.cL & 63u : 0u, C.Z);
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const bool live = k < B.nch;
     const bool can = live && p >= 1u && p <= B.mstart && B.n >= kMinLength;
@@ -342,11 +386,11 @@ __device__ __forceinline__ void p_measure(EncLds &S, const Blk &B, int k, int la
     const uint32_t P = 64u * (uint32_t)k;
     C.q2 = act ? (j | (seg << 8)) : 0xFFFFFFFFu;
     C.lg = lg;
-    // own segment p_j + 12 + 16 seg, candidate segment c + 12 + 16 seg (16 bytes each);
-    // idle lanes load the block start
-    const int po = act ? (int)(P + j + kM1 + 16u * seg) : 0;
+    // own segment p_j + 12 + 16 seg from the chunk image (byte j + 16 + 16 seg <= 127),
+    // candidate segment c + 12 + 16 seg (16 bytes each); idle lanes load the block start
+    x_window(S.xw[k & 1], act ? j + kM1 + 4u + 16u * seg : 0u, C.A);
+    (void)P;
     const int pc = act ? (int)(cc + kM1 + 16u * seg) : 0;
-    load16<SMALL>(B.in, B.n, po, C.A, FAST);
     load16<SMALL>(B.in, B.n, pc, C.Bc, FAST);
 }
 
@@ -449,10 +493,9 @@ __device__ __forceinline__ bool lane_bit(uint64_t m) {
 // match, :623-627) and every lane whether a match covers it; the members' sequences
 // then move to the next free lanes of the queue registers through a small LDS buffer,
 // so the emitter later writes 64 sequences per pass.
-__device__ __forceinline__ void walk_chain(EncLds &S, const Blk &B, int k, int lane, Walk &W,
-                                           WalkOut &O) {
+__device__ __forceinline__ void walk_chain(const Blk &B, int k, int lane, Walk &W, WalkOut &O,
+                                           const uint2 iv) {
     const uint32_t P = 64u * (uint32_t)k;
-    const uint2 iv = S.info[k % kNI][lane];
     O.x = iv.x;
     O.y = iv.y;
     O.walked = O.member = false;
@@ -665,22 +708,32 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
 
     if (wave == 1) {   // producer
         PSet C0, C1;
-        // one producer step; `cur` = set of chunks s and s + 2, `nxt` = s - 1 and s + 1
+        uint32_t XS = 0;   // chunk dword of the chunk in flight between L(k) and H(k)
+        // Load waits (vmcnt counts a wave's loads in issue order).  Issue order per step
+        // s: first half Y(s+1) X(s+2), second half Bc(s) -- one load instruction each
+        // outside SMALL (whose byte loads are waited for whole).
+        // H(s+1): X(s+1) is followed by Bc(s-1): 1 younger.
+        // F(s-1), then M(s): Bc(s-1) (and the older Y(s)) are followed by Y(s+1) X(s+2):
+        // 2 younger.  The step is two halves: H and F run beside the walker's chain, M
+        // beside its table inserts.
+        constexpr int kW1 = SMALL ? 0 : 1, kW2 = SMALL ? 0 : 2;
         auto pstep = [&](auto fast, int s, PSet &cur, PSet &nxt) {
             constexpr bool F = decltype(fast)::value;
-            // In flight, oldest first: Y/Z(s), A/Bc(s-1), X(s+1).
             // First half: H(s+1) -- the table reads (the walker inserts in second halves)
-            vm_wait<0>();                      // X(s+1)
+            vm_wait<kW1>();                    // X(s+1)
+            x_spread(S, s + 1, lane, XS, nxt.X);
             p_lookup<SMALL, F>(S, B, s + 1, lane, nxt);
+            p_load<SMALL, F>(B, s + 2, lane, XS);
+            // F(s-1) (info of chunk s-1: read by the walker in step s+1)
+            vm_wait<kW2>();                    // A/Bc(s-1), Y/Z(s)
+            p_finish(S, B, s - 1, lane, nxt);
             STAT(5);
             __builtin_amdgcn_sched_barrier(0);
             __syncthreads();
             STAT(6);
             __builtin_amdgcn_sched_barrier(0);
-            // Second half: M(s), L(s+2), F(s-1)
+            // Second half: M(s)
             p_measure<SMALL, F>(S, B, s, lane, cur);
-            p_load<SMALL, F>(B, s + 2, lane, cur.X);
-            p_finish(S, B, s - 1, lane, nxt);
 #ifdef APE_FINE_STATS
             STAT(8);
 #endif
@@ -693,19 +746,22 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             __builtin_amdgcn_sched_barrier(0);
         };
         if (k0 > 0) prefix_history(S, B, lane);
-        // prologue: in flight at the loop entry Y/Z(k0), A/Bc(k0-1) (idle, in C1), X(k0+1)
-        p_load<SMALL, false>(B, k0, lane, C0.X);
+        // prologue: the loads in flight at the loop entry in the steady-state order --
+        // Y(k0), X(k0+1), Bc(k0-1) (idle stand-in)
+        p_load<SMALL, false>(B, k0, lane, XS);
         __builtin_amdgcn_s_waitcnt(0);
+        x_spread(S, k0, lane, XS, C0.X);
         p_lookup<SMALL, false>(S, B, k0, lane, C0);
+        p_load<SMALL, false>(B, k0 + 1, lane, XS);
         C1.q2 = 0xFFFFFFFFu;
         C1.lg = 0;
-        load16<SMALL>(B.in, B.n, 0, C1.A, !SMALL);
+#pragma unroll
+        for (int t = 0; t < 4; t++) C1.A[t] = 0;
         load16<SMALL>(B.in, B.n, 0, C1.Bc, !SMALL);
-        p_load<SMALL, false>(B, k0 + 1, lane, C1.X);
         __syncthreads();   // table cleared, scratch ready
         // Steps whose loads all lie inside the block run a loop without edge paths:
-        // X(s+2): 64(s+2)+76 <= n; stage 2 of chunk s: 64s + 63 + 12 + 64 <= n.
-        const int nfast = SMALL || B.n < 204 ? 0 : (B.n - 204) / 64 + 1;
+        // X(s+2): 64(s+2)+140 <= n (stage 2 of chunk s reads c + 76 < p + 76 <= n).
+        const int nfast = SMALL || B.n < 268 ? 0 : (B.n - 268) / 64 + 1;
         int s = k0;
         // the first step always runs the edge path (chunk k0's backward context)
         pstep(std::false_type{}, s, C0, C1);
@@ -736,15 +792,17 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         WalkOut O;
         O.member = O.walked = false;
         O.x = O.y = 0;
+        uint2 iv = make_uint2(0u, 0u);   // info of the chunk walked next (read a half early)
         __syncthreads();
         for (int s = k0; s < nsteps; s++) {
-            // chunk s-2 is final: M(s-2) and F(s-2) ran in the second halves of steps
-            // s-2 and s-1
+            // chunk s-2 is final: M(s-2) ran in the second half of step s-2, F(s-2) in the
+            // first half of step s-1; its info was read in the second half of step s-1
             const bool work = s >= k0 + 2 && s - 2 < nch;
-            if (work) walk_chain(S, B, s - 2, lane, W, O);
+            if (work) walk_chain(B, s - 2, lane, W, O, iv);
             STAT(0);
             __syncthreads();
             STAT(4);
+            iv = S.info[(s - 1) & (kNI - 1)][lane];   // chunk s-1: final since F(s-1) above
             if (work) {
                 walk_post(S, s - 2, lane, W, O);
                 walk_publish(S, B, s - 2, lane, O);
