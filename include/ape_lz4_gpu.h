@@ -19,7 +19,8 @@
  *
  * Pointers named d_* are device pointers (hipMalloc / torch CUDA tensors).
  * `stream` is a hipStream_t passed as void* (NULL = default stream).  All
- * launchers are asynchronous and graph-capturable (no allocation, no sync).
+ * launchers are asynchronous and graph-capturable (no allocation, no sync), except
+ * APE_LZ4_compress_destSize_batch_dev (stream-ordered scratch; see its _scratch form).
  * Return value of a launcher: 0 on success, otherwise a negative
  * APE_LZ4_GPU_E* code (nothing was launched); per-block status is in d_result.
  *
@@ -119,11 +120,20 @@ int APE_LZ4_decompress_fast_batch_dev(const char *const *d_src, const int *d_src
  * valid LZ4 block of src[0, consumed) (decodes with cap = consumed); when the whole block
  * fits the target it is compress_default's output.  Bytes and consumed size differ from
  * the reference's greedy cut (the GPU parse is chunk-parallel; the cut is at a sequence
- * boundary followed by as many literals as fit).  Uses stream-ordered scratch of
- * ~65.8 KB per block, at most 16384 blocks at a time. */
+ * boundary followed by as many literals as fit).  The one launcher that allocates:
+ * stream-ordered scratch (hipMallocAsync/hipFreeAsync on `stream`) of ~65.8 KB per
+ * block, at most 16384 blocks at a time -- not for graph capture; the _scratch form
+ * below takes caller-owned scratch instead and allocates nothing. */
 int APE_LZ4_compress_destSize_batch_dev(const char *const *d_src, int *d_srcSize,
                                         char *const *d_dst, const int *d_targetDstSize,
                                         int *d_result, int nblocks, void *stream);
+/* Scratch bytes for destSize of nblocks in one pass (a smaller 16-aligned scratch, at
+ * least scratch_size(1), makes the call run several passes). */
+size_t APE_LZ4_compress_destSize_scratch_size(int nblocks);
+int APE_LZ4_compress_destSize_batch_scratch_dev(const char *const *d_src, int *d_srcSize,
+                                                char *const *d_dst, const int *d_targetDstSize,
+                                                int *d_result, int nblocks, void *d_scratch,
+                                                size_t scratch_bytes, void *stream);
 
 /* ---- batched, device-resident, strided form (block i at base + i*stride) ----
  * The layout the benchmark uses: uncompressed slots of `src_stride` bytes,

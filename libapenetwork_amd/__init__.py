@@ -19,6 +19,7 @@ __all__ = [
     "MAX_BLOCK", "ERANGE", "frame_offsets", "frame_pack", "decompress_frames",
     "compress_prefix_batch", "decompress_dict_batch", "compress_fast_ptr_batch",
     "decompress_fast_ptr_batch", "compress_destSize_ptr_batch", "RxBuf",
+    "compress_destSize_scratch_ptr_batch", "destSize_scratch_size",
     "socket_send_blocks", "socket_recv_blocks",
 ]
 
@@ -58,6 +59,8 @@ def lib():
             "APE_LZ4_compress_batch_dev": (i, [p, p, p, p, p, i, p]),
             "APE_LZ4_compress_fast_batch_dev": (i, [p, p, p, p, p, i, i, p]),
             "APE_LZ4_compress_destSize_batch_dev": (i, [p, p, p, p, p, i, p]),
+            "APE_LZ4_compress_destSize_scratch_size": (sz, [i]),
+            "APE_LZ4_compress_destSize_batch_scratch_dev": (i, [p, p, p, p, p, i, p, sz, p]),
             "APE_LZ4_decompress_fast_batch_dev": (i, [p, p, p, p, p, i, p]),
             "APE_LZ4_decompress_safe_batch_dev": (i, [p, p, p, p, p, i, p]),
             "APE_LZ4_decompress_safe_partial_batch_dev": (i, [p, p, p, p, p, p, i, p]),
@@ -202,6 +205,21 @@ def compress_destSize_ptr_batch(src_ptrs, src_sizes, dst_ptrs, targets, results,
     _check(lib().APE_LZ4_compress_destSize_batch_dev(
         _ptr(src_ptrs), _ptr(src_sizes), _ptr(dst_ptrs), _ptr(targets), _ptr(results), n,
         _stream(stream)), "APE_LZ4_compress_destSize_batch_dev")
+
+
+def compress_destSize_scratch_ptr_batch(src_ptrs, src_sizes, dst_ptrs, targets, results,
+                                        scratch, stream=None):
+    """compress_destSize_ptr_batch with caller-owned scratch (uint8 CUDA tensor of at least
+    destSize_scratch_size(1) bytes): allocates nothing, so it can be graph-captured."""
+    n = src_sizes.shape[0]
+    _check(lib().APE_LZ4_compress_destSize_batch_scratch_dev(
+        _ptr(src_ptrs), _ptr(src_sizes), _ptr(dst_ptrs), _ptr(targets), _ptr(results), n,
+        _ptr(scratch), scratch.numel(), _stream(stream)),
+        "APE_LZ4_compress_destSize_batch_scratch_dev")
+
+
+def destSize_scratch_size(nblocks):
+    return lib().APE_LZ4_compress_destSize_scratch_size(nblocks)
 
 
 def decompress_fast_ptr_batch(src_ptrs, src_bounds, dst_ptrs, original_sizes, results,

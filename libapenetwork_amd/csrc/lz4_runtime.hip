@@ -375,28 +375,20 @@ int APE_LZ4_compress_withPrefix_batch_dev(const char *const *d_src, const int *d
     return finish_launch(launch_encode(a, (hipStream_t)stream), "lz4_encode_kernel<prefix>");
 }
 
-int APE_LZ4_compress_destSize_batch_dev(const char *const *d_src, int *d_srcSize,
-                                        char *const *d_dst, const int *d_targetDstSize,
-                                        int *d_result, int nblocks, void *stream) {
-    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_srcSize || !d_dst || !d_targetDstSize ||
-                                         !d_result)))
-        return APE_LZ4_GPU_EINVAL;
-    int rc = check_device();
-    if (rc) return rc;
-    if (nblocks == 0) return APE_LZ4_GPU_OK;
-    // scratch: full-size encoder output for up to kSub blocks at a time, stream-ordered
-    // (allocated and freed on the caller's stream, so concurrent calls never share it)
-    constexpr int kSub = 16384;
-    const size_t stride = up16((size_t)kMaxBlock + kMaxBlock / 255 + 16);
-    const int sub = nblocks < kSub ? nblocks : kSub;
-    hipStream_t s = (hipStream_t)stream;
-    char *scr = nullptr;
-    hipError_t e = hipMallocAsync((void **)&scr, (size_t)sub * stride + (size_t)sub * sizeof(int), s);
-    if (e != hipSuccess) {
-        set_err("hipMallocAsync (destSize scratch)", e);
-        return APE_LZ4_GPU_ENOMEM;
-    }
+namespace {
+
+constexpr int kDsSub = 16384;   // destSize: blocks per scratch pass
+inline size_t ds_stride() { return up16((size_t)kMaxBlock + kMaxBlock / 255 + 16); }
+inline size_t ds_scratch(int sub) { return (size_t)sub * ds_stride() + (size_t)sub * sizeof(int); }
+
+// encode into the scratch (full-size output, every block fits), then cut each block to
+// its target; `sub` blocks per pass (the scratch holds ds_scratch(sub) bytes)
+hipError_t destsize_passes(const char *const *d_src, int *d_srcSize, char *const *d_dst,
+                           const int *d_targetDstSize, int *d_result, int nblocks, char *scr,
+                           int sub, hipStream_t s) {
+    const size_t stride = ds_stride();
     int *sres = (int *)(scr + (size_t)sub * stride);
+    hipError_t e = hipSuccess;
     for (int off = 0; off < nblocks && e == hipSuccess; off += sub) {
         const int m = nblocks - off < sub ? nblocks - off : sub;
         BlockArgs a{};
@@ -411,6 +403,61 @@ int APE_LZ4_compress_destSize_batch_dev(const char *const *d_src, int *d_srcSize
             e = launch_destsize(d_src + off, d_srcSize + off, d_dst + off, d_targetDstSize + off,
                                 d_result + off, scr, stride, sres, m, s);
     }
+    return e;
+}
+
+}  // namespace
+
+size_t APE_LZ4_compress_destSize_scratch_size(int nblocks) {
+    const int sub = nblocks < 1 ? 1 : (nblocks < kDsSub ? nblocks : kDsSub);
+    return ds_scratch(sub);
+}
+
+int APE_LZ4_compress_destSize_batch_scratch_dev(const char *const *d_src, int *d_srcSize,
+                                                char *const *d_dst, const int *d_targetDstSize,
+                                                int *d_result, int nblocks, void *d_scratch,
+                                                size_t scratch_bytes, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_srcSize || !d_dst || !d_targetDstSize ||
+                                         !d_result || !d_scratch)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    if (nblocks == 0) return APE_LZ4_GPU_OK;
+    // as many blocks per pass as the caller's scratch holds (at least one)
+    int sub = (int)(scratch_bytes / (ds_stride() + sizeof(int)));
+    if (sub < 1) {
+        snprintf(g_err, sizeof g_err, "destSize scratch of %zu bytes < %zu (one block)",
+                 scratch_bytes, ds_scratch(1));
+        return APE_LZ4_GPU_EINVAL;
+    }
+    if (sub > nblocks) sub = nblocks;
+    if ((uintptr_t)d_scratch & 15u) return APE_LZ4_GPU_EINVAL;
+    return finish_launch(destsize_passes(d_src, d_srcSize, d_dst, d_targetDstSize, d_result,
+                                         nblocks, (char *)d_scratch, sub, (hipStream_t)stream),
+                         "lz4_encode_kernel + lz4_destsize_kernel");
+}
+
+int APE_LZ4_compress_destSize_batch_dev(const char *const *d_src, int *d_srcSize,
+                                        char *const *d_dst, const int *d_targetDstSize,
+                                        int *d_result, int nblocks, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_srcSize || !d_dst || !d_targetDstSize ||
+                                         !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    if (nblocks == 0) return APE_LZ4_GPU_OK;
+    // The one launcher that allocates: stream-ordered scratch (hipMallocAsync / hipFreeAsync
+    // on the caller's stream, so concurrent calls never share it).  Under graph capture
+    // use APE_LZ4_compress_destSize_batch_scratch_dev with caller-owned scratch.
+    const int sub = nblocks < kDsSub ? nblocks : kDsSub;
+    hipStream_t s = (hipStream_t)stream;
+    char *scr = nullptr;
+    hipError_t e = hipMallocAsync((void **)&scr, ds_scratch(sub), s);
+    if (e != hipSuccess) {
+        set_err("hipMallocAsync (destSize scratch)", e);
+        return APE_LZ4_GPU_ENOMEM;
+    }
+    e = destsize_passes(d_src, d_srcSize, d_dst, d_targetDstSize, d_result, nblocks, scr, sub, s);
     hipError_t ef = hipFreeAsync(scr, s);
     if (e == hipSuccess) e = ef;
     return finish_launch(e, "lz4_encode_kernel + lz4_destsize_kernel");

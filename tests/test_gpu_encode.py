@@ -194,3 +194,48 @@ def test_destsize(cuda, product, oracle):
     print("destSize consumed: GPU %d vs reference %d (%.4f)" % (gpu_sum, ref_sum,
                                                                gpu_sum / ref_sum))
     assert gpu_sum >= 0.95 * ref_sum
+
+
+@pytest.mark.gpu
+def test_destSize_scratch_form_matches_and_captures(cuda, product, oracle):
+    """APE_LZ4_compress_destSize_batch_scratch_dev (caller-owned scratch, no allocation):
+    the same results as the allocating form, with one-block scratch (a pass per block)
+    and inside a captured HIP graph replayed twice."""
+    srcs = [I.synth_comp(65536, b) for b in range(5)] + [I.make("text", 4096, seed=3)]
+    tgts = [20000, 1000, 30000, 5000, 17, 600]
+    src, sptr, _ = pack(cuda, srcs)
+    tg = ints(cuda, tgts)
+
+    def run(mode):
+        dst, dptr, doffs = alloc_out(cuda, tgts)
+        sizes = ints(cuda, map(len, srcs))
+        res = ints(cuda, [-7] * len(srcs))
+        if mode == "alloc":
+            product.compress_destSize_ptr_batch(sptr, sizes, dptr, tg, res)
+        else:
+            nb = 1 if mode == "one" else len(srcs)
+            scr = cuda.empty(product.destSize_scratch_size(nb), dtype=cuda.uint8, device="cuda")
+            if mode == "graph":
+                s = cuda.cuda.Stream()
+                s.wait_stream(cuda.cuda.current_stream())
+                g = cuda.cuda.CUDAGraph()
+                sz0 = sizes.clone()
+                with cuda.cuda.graph(g, stream=s):
+                    product.compress_destSize_scratch_ptr_batch(sptr, sizes, dptr, tg, res, scr,
+                                                                stream=s)
+                for _ in range(2):
+                    sizes.copy_(sz0)
+                    g.replay()
+            else:
+                product.compress_destSize_scratch_ptr_batch(sptr, sizes, dptr, tg, res, scr)
+        cuda.cuda.synchronize()
+        rs, ks = res.cpu().tolist(), sizes.cpu().tolist()
+        return rs, ks, [fetch(dst, o, max(r, 0)) for o, r in zip(doffs, rs)]
+
+    ref = run("alloc")
+    for mode in ("one", "all", "graph"):
+        assert run(mode) == ref, mode
+    for s, r, k, c in zip(srcs, *ref):
+        assert r > 0
+        dr, out = orc_decompress(oracle, c, k)
+        assert dr == k and out == s[:k]
