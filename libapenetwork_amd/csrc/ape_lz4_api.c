@@ -49,11 +49,43 @@ static int host_compress(void *state, const char *src, char *dst, int n, int cap
     return hst_compress_extstate(state ? (hst_stream *)state : &st, src, dst, n, cap, accel);
 }
 
+/* Opt-in latency routing ("a kernel launch costs more than one block").
+ * One call of the GPU one-shot path is a pinned copy, H2D, one workgroup working through
+ * the block's 1024 chunks, D2H and a stream sync: measured 39 / 126 / 848 us to compress
+ * 1 / 8 / 64 KiB (decompress 45 / 112 / 784 us), against 5 / 6 / 47 us (2 / 3 / 15 us)
+ * for the reference algorithm on one host core (tests/test_gpu_api.py).  The
+ * GPU pays off only for many blocks at once -- the batch entry points.  The library's
+ * contract stays "the codec runs on the GPU" (default threshold 0), so a missing GPU
+ * fails loudly; a caller with single latency-bound blocks sets a threshold (API or
+ * APE_LZ4_ONESHOT_HOST_BELOW), and one-shot calls on smaller blocks (compress: input
+ * size; decompress: capacity) then run the host codec, byte-identical to the reference. */
+static int g_host_below = -1;
+
+static int host_below(void)
+{
+    int v = __atomic_load_n(&g_host_below, __ATOMIC_RELAXED);
+    if (v < 0) {
+        const char *e = getenv("APE_LZ4_ONESHOT_HOST_BELOW");
+        v = e ? atoi(e) : 0;
+        if (v < 0) v = 0;
+        __atomic_store_n(&g_host_below, v, __ATOMIC_RELAXED);
+    }
+    return v;
+}
+
+int APE_LZ4_gpu_set_oneshot_host_below(int bytes)
+{
+    const int prev = host_below();
+    __atomic_store_n(&g_host_below, bytes < 0 ? 0 : bytes, __ATOMIC_RELAXED);
+    return prev;
+}
+
 static int gpu_compress_st(void *state, const char *src, char *dst, int n, int cap, int accel)
 {
     int rt = 0, r;
     if ((unsigned)n > (unsigned)LZ4_MAX_INPUT_SIZE) return 0; /* ref :558 */
-    if (n > APE_LZ4_GPU_MAX_BLOCK) return host_compress(state, src, dst, n, cap, accel);
+    if (n > APE_LZ4_GPU_MAX_BLOCK || n < host_below())
+        return host_compress(state, src, dst, n, cap, accel);
     r = ape_lz4_gpu_compress_one(src, dst, n, cap, accel, &rt);
     if (rt) { gpu_failed(rt); return 0; }
     return r == APE_LZ4_GPU_ERANGE ? 0 : r;
@@ -66,7 +98,10 @@ static int gpu_compress(const char *src, char *dst, int n, int cap, int accel)
 
 static int gpu_decompress(const char *src, char *dst, int csize, int cap, int partial, int target)
 {
-    int rt = 0, r = ape_lz4_gpu_decompress_one(src, dst, csize, cap, partial, target, &rt);
+    int rt = 0, r;
+    if (cap >= 0 && cap < host_below())
+        return hst_decompress_block(src, dst, csize, cap, partial, target);
+    r = ape_lz4_gpu_decompress_one(src, dst, csize, cap, partial, target, &rt);
     if (rt) { gpu_failed(rt); return -1; }
     return r;
 }

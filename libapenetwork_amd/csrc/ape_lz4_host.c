@@ -575,6 +575,13 @@ int hst_decompress_safe_extdict(const char *s, char *d, int csize, int cap, cons
                        (const byte *)dict, (size_t)dsize);
 }
 
+/* decompress_safe / _safe_partial of one block without a dictionary (ref :1472-1487) */
+int hst_decompress_block(const char *s, char *d, int csize, int cap, int partial, int target)
+{
+    return decode_core((const byte *)s, (byte *)d, csize, cap, 1, partial, target, 0,
+                       (const byte *)d, NULL, 0);
+}
+
 int hst_decompress_usingDict(const char *s, char *d, int csize, int cap, int safe,
                              const char *dict, int dsize)
 {

@@ -35,6 +35,7 @@ int hst_compress_continue(hst_stream *d, const char *src, char *dst, int n, int 
 int hst_compress_forceExtDict(hst_stream *d, const char *src, char *dst, int n);
 int hst_saveDict(hst_stream *d, char *safe, int size);
 int hst_decompress_fast(const char *s, char *d, int osize);
+int hst_decompress_block(const char *s, char *d, int csize, int cap, int partial, int target);
 int hst_decompress_safe_prefix64k(const char *s, char *d, int csize, int cap);
 int hst_decompress_safe_extdict(const char *s, char *d, int csize, int cap, const char *dict,
                                 int dsize);

@@ -136,12 +136,13 @@ def test_concurrent_one_shot_callers(cuda, product, oracle):
     assert not errors, errors[:5]
 
 
-def test_one_shot_latency_recorded(cuda, product):
-    """One-call latency of the GPU one-shot path next to the host codec, for the routing
-    note in DESIGN.md: printed, and sanity-bounded only."""
+def test_one_shot_latency_recorded(cuda, product, oracle):
+    """One-call latency of the GPU one-shot path next to the reference algorithm on one
+    host core (the oracle restatement, as the checker's clock), for the routing note in
+    DESIGN.md: printed, and sanity-bounded only."""
     import time
     L = product.lib()
-    for n in (4096, 65536):
+    for n in (1024, 8192, 65536):
         s = I.make("comp", n, seed=5)
         o = C.create_string_buffer(product.compressBound(n) + 64)
         b = buf(s)
@@ -157,5 +158,15 @@ def test_one_shot_latency_recorded(cuda, product):
         for _ in range(20):
             L.APE_LZ4_decompress_safe(cb, d, r, n)
         dd = (time.perf_counter() - t0) / 20
-        print("one-shot n=%d: compress %.1f us, decompress %.1f us" % (n, dt * 1e6, dd * 1e6))
+        t0 = time.perf_counter()
+        for _ in range(20):
+            orc_compress(oracle, s)
+        hc = (time.perf_counter() - t0) / 20
+        t0 = time.perf_counter()
+        for _ in range(20):
+            orc_decompress(oracle, o.raw[:r], n)
+        hd = (time.perf_counter() - t0) / 20
+        print("one-shot n=%d: GPU compress %.1f us, decompress %.1f us | one host core "
+              "(reference algorithm): compress %.1f us, decompress %.1f us" % (
+                  n, dt * 1e6, dd * 1e6, hc * 1e6, hd * 1e6))
         assert dt < 0.5 and dd < 0.5

@@ -226,3 +226,37 @@ def test_one_shot_compress_above_gpu_block(product, golden, oracle):
         out2 = C.create_string_buffer(bound + 64)
         assert L.APE_LZ4_compress_fast_extState(state, buf(src), out2, n, bound, 1) == er
         assert out2.raw[:er] == eout
+
+
+def test_oneshot_host_routing_threshold(product, golden):
+    """APE_LZ4_gpu_set_oneshot_host_below (opt-in latency routing): below the
+    threshold the one-shot calls run the host codec and return the reference's exact
+    results -- compress bytes, decompress_safe and _partial return values and bytes --
+    GPU or not; the default (0) keeps every one-shot call on the GPU."""
+    import base64
+    from lz4util import blob_matches
+    L = product.lib()
+    L.APE_LZ4_gpu_set_oneshot_host_below.restype = C.c_int
+    L.APE_LZ4_gpu_set_oneshot_host_below.argtypes = [C.c_int]
+    prev = L.APE_LZ4_gpu_set_oneshot_host_below(1 << 30)
+    try:
+        assert prev == 0
+        for e in golden["encode"]:
+            if e["n"] > 65536:
+                continue
+            src = I.make(e["content"], e["n"])
+            out = C.create_string_buffer(e["bound"] + 64)
+            r = L.APE_LZ4_compress_default(buf(src), out, e["n"], e["bound"])
+            assert r == e["clen"] and blob_matches(e["comp"], out.raw[:r]), (e["content"], e["n"])
+        for d in golden["decode"]:
+            comp = base64.b64decode(d["comp_b64"])
+            r, out = product.decompress_safe(comp, d["cap"])
+            assert r == d["ret"], d["name"]
+            if r > 0 and not d["has_offset0"]:
+                assert sha(out) == d["out_sha256"], d["name"]
+            pr, _ = product.decompress_safe_partial(comp, d["partial"]["target"], d["cap"])
+            assert pr == d["partial"]["ret"], d["name"]
+    finally:
+        assert L.APE_LZ4_gpu_set_oneshot_host_below(prev) == 1 << 30
+    if L.APE_LZ4_gpu_device_count() == 0:   # back on the GPU path: fails loudly here
+        assert product.compress_default(b"hello hello hello hello hello")[0] == 0
