@@ -274,6 +274,8 @@ struct Blk {
                                      // history prefix (withPrefix encode), only hashed
     uint32_t nr;                     // bytes to encode (n - 64 k0)
     bool noL;                        // acceleration > 1: no in-chunk candidate
+    uint32_t stride;                 // acceleration: search every stride-th position
+    uint64_t pat;                    // bits 0, stride, 2 stride, ... (< 64)
 };
 
 // ---------------- producer ----------------
@@ -421,8 +423,9 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
 
 // ---------------- walker ----------------
 struct Walk {
-    uint32_t q;          // walk position
+    uint32_t q;          // walk position (the next probe)
     uint32_t anchor;     // start of the pending literals
+    uint32_t dense;      // acceleration: consecutive probes left before the stride phase
 };
 
 // forward extension of the match at m (candidate cm) from L bytes on, with the
@@ -498,8 +501,27 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     uint32_t rel = W.q - P;
     uint64_t M = 0;
     for (;;) {
-        const uint64_t w = Hm >> rel;
-        if (w == 0) { rel = 64u; break; }
+        // acceleration (:591-600): after a match end e the reference tests e (:710-720),
+        // then searches from e+1 with step 1 once and then step = acceleration (without
+        // the growth after 64 misses): probes e, e+1, e+2, e+2+a, e+2+2a, ...  `dense`
+        // = consecutive probes left from rel; then every stride-th.
+        const uint32_t dn = W.dense;
+        const uint64_t pm = B.stride == 1u ? ~0ull
+                                           : (dn ? ((1ull << dn) - 1ull) | (B.pat << (dn - 1u)) : B.pat);
+        const uint64_t w = (Hm >> rel) & pm;
+        if (w == 0) {   // next probe position past the chunk
+            if (B.stride == 1u) {
+                rel = 64u;
+            } else if (rel + dn > 64u) {          // still in the consecutive probes
+                W.dense = rel + dn - 64u;
+                rel = 64u;
+            } else {
+                const uint32_t b = dn ? rel + dn - 1u : rel;   // the stride phase's base
+                rel = b + ((64u - b + B.stride - 1u) / B.stride) * B.stride;
+                W.dense = 0;
+            }
+            break;
+        }
         const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
         const uint32_t h = lane_val(Lh, (int)j);
         M |= 1ull << j;
@@ -512,13 +534,14 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
         } else {
             rel = j + h;
         }
+        W.dense = 3u;   // a new search from the match end
         if (rel >= 64u) break;
     }
     O.members = M;
     W.q = P + rel;
 }
 
-__device__ __forceinline__ void walk_finish(int k, int lane, Walk &W, WalkOut &O) {
+__device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk &W, WalkOut &O) {
     const uint32_t P = 64u * (uint32_t)k;
     if (O.q0 >= P + 64u) return;              // covered by a match from earlier chunks
     // catch-up limits: a member's backward extension stops at the previous end
@@ -533,7 +556,10 @@ __device__ __forceinline__ void walk_finish(int k, int lane, Walk &W, WalkOut &O
     O.m_len = O.Lf + bk;
     O.an = pm;
     // walked = every position from the walk start that no match of this chunk covers
-    O.walked = wave_ballot(p >= umax(O.q0, pm));
+    // (with acceleration: the probed ones, every stride-th from the last match end)
+    bool w = p >= umax(O.q0, pm);
+    if (B.stride > 1u) w = w && (p - pm < 3u || (p - pm - 2u) % B.stride == 0u);
+    O.walked = wave_ballot(w);
     W.anchor = umax(anchor0, lane_val(imax, 63));
 }
 
@@ -791,6 +817,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         Walk W;
         W.q = 64u * (uint32_t)k0;
         W.anchor = W.q;
+        W.dense = 3u;   // the first search probes 0, 1, 2, then every stride-th
         WalkOut O;
         __syncthreads();
         for (int s = k0; s < nsteps; s++) {
@@ -800,7 +827,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             __syncthreads();
             STAT(4);
             if (work) {
-                walk_finish(s - 1, lane, W, O);
+                walk_finish(B, s - 1, lane, W, O);
                 walk_publish(S, B, s - 1, lane, O);
                 STAT_ADD(11, __popcll(O.members));
             }
@@ -924,6 +951,9 @@ lz4_encode_v1_kernel(BlockArgs a) {
     // compress_fast's acceleration (:789-808) trades ratio for speed; here that is the
     // in-chunk candidate (-11 % encode time, ratio -1.7 % on App. C data)
     B.noL = a.accel > 1;
+    B.stride = a.accel > 1 ? (a.accel < (1 << 20) ? (uint32_t)a.accel : 1u << 20) : 1u;
+    B.pat = 0;
+    for (uint32_t i = 0; i < 64u; i += B.stride) B.pat |= 1ull << i;
     B.cap = (uint32_t)icap;
     B.un = (uint32_t)B.n;
     B.mstart = B.un >= 12 ? B.un - 12 : 0;   // matches start at <= n-12 (:585)
