@@ -485,6 +485,7 @@ struct WalkOut {
 
 // First half: the hop chain only (the latency-bound part); second half, before the
 // inserts: the lane-parallel catch-up limits, walked set and anchor (walk_finish).
+template <bool ACC>
 __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k, int lane, Walk &W,
                                            WalkOut &O) {
     const uint32_t P = 64u * (uint32_t)k;
@@ -506,11 +507,11 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
         // the growth after 64 misses): probes e, e+1, e+2, e+2+a, e+2+2a, ...  `dense`
         // = consecutive probes left from rel; then every stride-th.
         const uint32_t dn = W.dense;
-        const uint64_t pm = B.stride == 1u ? ~0ull
-                                           : (dn ? ((1ull << dn) - 1ull) | (B.pat << (dn - 1u)) : B.pat);
+        const uint64_t pm = !ACC ? ~0ull
+                                 : (dn ? ((1ull << dn) - 1ull) | (B.pat << (dn - 1u)) : B.pat);
         const uint64_t w = (Hm >> rel) & pm;
         if (w == 0) {   // next probe position past the chunk
-            if (B.stride == 1u) {
+            if (!ACC) {
                 rel = 64u;
             } else if (rel + dn > 64u) {          // still in the consecutive probes
                 W.dense = rel + dn - 64u;
@@ -534,13 +535,14 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
         } else {
             rel = j + h;
         }
-        W.dense = 3u;   // a new search from the match end
+        if (ACC) W.dense = 3u;   // a new search from the match end
         if (rel >= 64u) break;
     }
     O.members = M;
     W.q = P + rel;
 }
 
+template <bool ACC>
 __device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk &W, WalkOut &O) {
     const uint32_t P = 64u * (uint32_t)k;
     if (O.q0 >= P + 64u) return;              // covered by a match from earlier chunks
@@ -558,7 +560,7 @@ __device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk 
     // walked = every position from the walk start that no match of this chunk covers
     // (with acceleration: the probed ones, every stride-th from the last match end)
     bool w = p >= umax(O.q0, pm);
-    if (B.stride > 1u) w = w && (p - pm < 3u || (p - pm - 2u) % B.stride == 0u);
+    if (ACC) w = w && (p - pm < 3u || (p - pm - 2u) % B.stride == 0u);
     O.walked = wave_ballot(w);
     W.anchor = umax(anchor0, lane_val(imax, 63));
 }
@@ -747,7 +749,7 @@ __device__ __forceinline__ void prefix_history(EncLds &S, const Blk &B, int lane
 //   step s, second half: producer C2(s) -> info[s%3]     | walker inserts s-1, publishes
 //                                                         | emitter sizes s-2
 // Table inserts (second half) never overlap the producer's lookups (first half).
-template <bool SMALL>
+template <bool SMALL, bool ACC>
 __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, int lane,
                                              int *result) {
     STATS_DECL
@@ -822,12 +824,12 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         __syncthreads();
         for (int s = k0; s < nsteps; s++) {
             const bool work = s >= k0 + 1 && s <= nch;
-            if (work) walk_chain(S, B, s - 1, lane, W, O);
+            if (work) walk_chain<ACC>(S, B, s - 1, lane, W, O);
             STAT(0);
             __syncthreads();
             STAT(4);
             if (work) {
-                walk_finish(B, s - 1, lane, W, O);
+                walk_finish<ACC>(B, s - 1, lane, W, O);
                 walk_publish(S, B, s - 1, lane, O);
                 STAT_ADD(11, __popcll(O.members));
             }
@@ -918,6 +920,9 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
 
 }  // namespace
 
+// ACC: compress_fast with acceleration > 1 (its own instantiation, so the default
+// kernel carries none of the probe-pattern code)
+template <bool ACC>
 __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(6)))
 lz4_encode_v1_kernel(BlockArgs a) {
     __shared__ EncLds S;
@@ -950,10 +955,11 @@ lz4_encode_v1_kernel(BlockArgs a) {
     B.k0 = D / 64;
     // compress_fast's acceleration (:789-808) trades ratio for speed; here that is the
     // in-chunk candidate (-11 % encode time, ratio -1.7 % on App. C data)
-    B.noL = a.accel > 1;
-    B.stride = a.accel > 1 ? (a.accel < (1 << 20) ? (uint32_t)a.accel : 1u << 20) : 1u;
+    B.noL = ACC;
+    B.stride = ACC ? (a.accel < (1 << 20) ? (uint32_t)a.accel : 1u << 20) : 1u;
     B.pat = 0;
-    for (uint32_t i = 0; i < 64u; i += B.stride) B.pat |= 1ull << i;
+    if (ACC)
+        for (uint32_t i = 0; i < 64u; i += B.stride) B.pat |= 1ull << i;
     B.cap = (uint32_t)icap;
     B.un = (uint32_t)B.n;
     B.mstart = B.un >= 12 ? B.un - 12 : 0;   // matches start at <= n-12 (:585)
@@ -966,13 +972,16 @@ lz4_encode_v1_kernel(BlockArgs a) {
     for (int i = tid; i < (int)(kRingE / 16 + 4); i += 192) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
     if (tid < 16) S.omap[tid] = 0u;
     __syncthreads();
-    if (B.n < kSmall) encode_block<true>(S, B, wave, lane, &a.result[b]);
-    else encode_block<false>(S, B, wave, lane, &a.result[b]);
+    if (B.n < kSmall) encode_block<true, ACC>(S, B, wave, lane, &a.result[b]);
+    else encode_block<false, ACC>(S, B, wave, lane, &a.result[b]);
 }
 
 hipError_t launch_encode_v1(const BlockArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(lz4_encode_v1_kernel, dim3(a.nblocks), dim3(192), 0, s, a);
+    if (a.accel > 1)
+        hipLaunchKernelGGL(lz4_encode_v1_kernel<true>, dim3(a.nblocks), dim3(192), 0, s, a);
+    else
+        hipLaunchKernelGGL(lz4_encode_v1_kernel<false>, dim3(a.nblocks), dim3(192), 0, s, a);
     return hipGetLastError();
 }
 
