@@ -56,6 +56,10 @@ constexpr uint32_t kEagerL = 12;     // ... for the in-chunk candidate L
 #define APE_LZ4_ERING 1024
 #endif
 constexpr uint32_t kRingE = APE_LZ4_ERING;  // recent input bytes (own, stage 2, end-2, literals)
+// Diagnostic A/B: with a 64 KiB ring the whole block window sits in LDS
+// and the candidate bytes (Y, E) are read from it instead of global memory -- 84 KiB
+// of LDS per block, one block per CU.  Never the product.
+constexpr bool kWin = kRingE >= 65536u;
 #ifndef APE_LZ4_SCRBITS
 #define APE_LZ4_SCRBITS 6
 #endif
@@ -351,7 +355,7 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
     // T candidate bytes (issued now, consumed one step later).  Candidates below
     // position 4 are skipped: their 4 bytes of backward context would start before
     // the block and need the slow edge path (never-written slots read as 0).
-    prod_fetch_t<SMALL, FAST>(B, k, lane, cT, Y);
+    if (!kWin) prod_fetch_t<SMALL, FAST>(B, k, lane, cT, Y);
 }
 
 // C1(k): verify / measure 28 bytes / pick; issue the second-stage load
@@ -362,6 +366,13 @@ __device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int 
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     uint32_t X[8];
     ring32(S, p - 4u, X);            // own bytes in[p-4, p+28) (ring tail = 0 before 0)
+    uint32_t Yw[8];
+    if (kWin) {   // candidate bytes from the LDS window (chunks <= k+1 are in it by now)
+        const bool tryT = k < B.nch && cT < p && cT >= 4u;
+        ring32(S, tryT ? cT - 4u : 0u, Yw);
+    }
+    const uint32_t (&Yr)[8] = kWin ? Yw : Y;
+#define Y Yr
     const bool live = k < B.nch;
     R.hashable = live && p + 5u <= B.un;
     const bool can = live && p >= 1u && p <= B.mstart && B.n >= kMinLength;
@@ -392,6 +403,11 @@ __device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int 
     R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
     R.has = okT || okL;
     R.h = h;
+#undef Y
+    if (kWin) {
+        ring32(S, R.trunc1 ? R.c + R.base : 0u, E);
+        return;
+    }
     load32<SMALL>(B.in, B.n, R.trunc1 ? (int)(R.c + R.base) : 0, E,
                   FAST || 64 * k + 123 <= B.n);
 }
@@ -768,17 +784,17 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             // from the block start and records nothing), so the number of loads per
             // step -- and with it the waits -- is the same on every path.
             // In flight, oldest first: A(s+2), Y(s+1) x2, E(s) x2 -> A(s+2) at 4.
-            vm_wait<4>();
+            vm_wait<kWin ? 0 : 4>();
             prod_load<SMALL, F>(B, s + 3, lane, nxt.X);
             prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
             // Y(s+1) x2, E(s) x2, A(s+3), Y(s+2) x2 -> Y(s+1) at 5
-            vm_wait<5>();
+            vm_wait<kWin ? 1 : 5>();
             prod_measure<SMALL, F>(S, B, s + 1, lane, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q, nxt.E);
             STAT(5);
             __syncthreads();
             STAT(6);
             // E(s) x2, A(s+3), Y(s+2) x2, E(s+1) x2 -> E(s) at 5
-            vm_wait<5>();
+            vm_wait<kWin ? 1 : 5>();
             prod_finish(S, B, s, lane, cur.q, cur.E);
             STAT(7);
             __syncthreads();
