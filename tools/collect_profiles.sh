@@ -1,12 +1,12 @@
 #!/bin/bash
 # Copy a refresh_profiles.sh run's results from gpurun_out/ into profiles/ (run here).
 set -e
-TAG=${1:-r1}
+TAG=${1:-r2}
 cd "$(dirname "$0")/.."
-cp gpurun_out/bench_$TAG.json profiles/r1_bench.json
-cp gpurun_out/prof_$TAG/run_kernel_stats.csv profiles/r1_kernel_stats.csv
-cp gpurun_out/stream_$TAG.json profiles/r1_stream.json
-cp gpurun_out/rand4k_$TAG.json profiles/r1_rand4k.json
-cp gpurun_out/e2e_$TAG.json profiles/r1_e2e.json
-python3 tools/sq_issue.py 16384
-python3 tools/pmc_traffic.py 65536
+cp gpurun_out/bench_$TAG.json profiles/${TAG}_bench.json
+cp gpurun_out/prof_$TAG/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
+for f in stream rand4k e2e sock; do
+  [ -f gpurun_out/${f}_$TAG.json ] && cp gpurun_out/${f}_$TAG.json profiles/${TAG}_$f.json
+done
+PROFILE_TAG=$TAG python3 tools/sq_issue.py 16384
+PROFILE_TAG=$TAG python3 tools/pmc_traffic.py 65536

@@ -2,7 +2,7 @@
 # Full bench.py line + rocprofv3 kernel stats of the same command (round profile).
 # usage: bash tools/gpu_bench.sh TAG
 set -o pipefail
-TAG=${1:-r1}
+TAG=${1:-r2}
 cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

@@ -4,10 +4,11 @@
 # of the same command, SQ issue passes, PMC FETCH_SIZE / WRITE_SIZE passes, and the
 # secondary bench lines (--stream, --rand4k, --e2e).
 set -o pipefail
-TAG=${1:-r1}
+TAG=${1:-r2}
 cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 bash tools/gpu_bench.sh $TAG || exit 1
+timeout -k 10 300 python3 -u bench.py --sock > gpurun_out/sock_$TAG.json 2> gpurun_out/sock_$TAG.err || exit 1
 bash tools/sq_passes.sh 16384 > gpurun_out/sq_$TAG.txt 2>&1 || { tail -5 gpurun_out/sq_$TAG.txt; exit 1; }
 NB=65536
 for c in FETCH_SIZE WRITE_SIZE; do

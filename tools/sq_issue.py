@@ -3,7 +3,7 @@
 
 Reads gpurun_out/sq/p*/run_{counter_collection,kernel_trace}.csv (16384 x 64 KiB blocks, one
 launch of each kernel) and writes profiles/sq_issue.json plus the raw counter CSVs
-(profiles/r1_sq_p1.csv, r1_sq_p2.csv).  Derived per kernel:
+(profiles/<tag>_sq_p1.csv, <tag>_sq_p2.csv; tag = $PROFILE_TAG, default r2).  Derived per kernel:
   valu_pipe_busy = SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves) / (SIMDs x cycles / 4)
   salu_busy, lds_busy: SQ_ACTIVE_INST_SCA / _LDS normalised the same way (per SIMD)
 with cycles = kernel duration x 2.4 GHz (MI355X_MICROARCH.md: max clock 2400 MHz; SQ_ACTIVE_INST_*
@@ -39,7 +39,7 @@ def main():
                     acc[(k, r["Counter_Name"])] += float(r["Counter_Value"])
             for (k, c), v in acc.items():
                 cnt[k][c] = v
-            shutil.copy(f, os.path.join(ROOT, "profiles", "r1_sq_%s.csv" % os.path.basename(p)))
+            shutil.copy(f, os.path.join(ROOT, "profiles", "%s_sq_%s.csv" % (os.environ.get("PROFILE_TAG", "r2"), os.path.basename(p))))
         for f in glob.glob(os.path.join(p, "*kernel_trace.csv")):
             for r in csv.DictReader(open(f)):
                 k = kind(r["Kernel_Name"])
