@@ -8,5 +8,5 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 400 python3 -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 1
 cat gpurun_out/bench_$TAG.json
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 -u bench.py --no-cpu-baseline > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/bench_prof_$TAG.err || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 -u bench.py --no-cpu-baseline --no-config2 --no-config5 > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/bench_prof_$TAG.err || exit 1
 cat gpurun_out/bench_prof_$TAG.json
