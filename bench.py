@@ -725,7 +725,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # APE_BENCH_DEVICE (rehearsal only): every rank on that device, to exercise the N > 1
+    # path on a one-GPU box; the driver's multi-GPU runs leave it unset
+    dev = os.environ.get("APE_BENCH_DEVICE")
+    torch.cuda.set_device(int(dev) if dev is not None else local)
     dist = None
     if world > 1:
         # no collective on the data path: the process group (gloo, host scalars) carries
