@@ -1,4 +1,6 @@
-// lz4_encode.hip -- MI355X (gfx950) batched LZ4 block encoder.
+// lz4_encode.hip -- MI355X (gfx950) batched LZ4 block encoder: the product encoder.
+// (lz4_encode_v2.hip is a second pipeline, selected by APE_LZ4_ENCODER=v2 for A/B
+// measurement; DESIGN.md 3.1.1 says why it is not the default.)
 //
 // Replaces the per-block work of APE_LZ4_compress_default (ref src/ape_lz4.c:
 // 811-815 -> LZ4_compress_generic :530-755, byU16 / noDict).  The output is a
@@ -9,36 +11,30 @@
 //
 // One 192-thread workgroup (three waves, one role each) per block; a batch holds
 // ~1M blocks, so most of the parallelism comes from many blocks in flight (8 per
-// CU).  Per block the LDS holds the reference's hash table (8192 x u16, 13-bit
-// hash of 5 bytes, :449-462) and the hand-over records between the roles.  The
-// block is cut into chunks of 64 positions, one per lane; the waves run in lock
-// step, two workgroup barriers per step s:
+// CU).  Per block the LDS (20.0 KiB) holds the reference's own hash table (8192 x
+// u16, 13-bit hash of 5 bytes, :449-462), a 1 KiB ring of recent input and the
+// hand-over records between the roles.  The input stays in HBM/L2.
 //
-//   PRODUCER (wave 1), four chunks in flight (every load is consumed one step after
-//   it is issued, so no wait ever covers a load of the same step):
-//     L(s+2)  load own bytes in[p-4, p+12) of every position p;
-//     H(s+1)  hash in[p, p+5), T = table[h] (positions walked earlier and
-//             match_end - 2, :595-619, :680-706), L = the earliest lane of the chunk
-//             with the same low hash bits; issue the loads of both candidates'
-//             bytes [c-4, c+12);
-//     M(s)    verify 4 bytes of T and L, measure both to 12 bytes and up to 4 bytes
-//             back (:623-627), keep the longer -> match record of chunk s.  Only
-//             the lanes whose match reached 12 bytes ("saturated", ~13 of 64 on the
-//             benchmark data) go on: they are compacted into a queue and each gets
-//             64 / 32 / 16 more bytes measured by 4 / 2 / 1 lanes (16 bytes per
-//             lane, issued now) -- the measurement work scales with the candidates
-//             that need it, not with the 64 positions;
-//     F(s-1)  finish those lengths (group minimum over the lanes of a candidate).
-//   WALKER (wave 0), chunk s-2: the greedy chain on the scalar unit -- a position
-//     with a match jumps past it, any other position is a literal -- with the
-//     catch-up limit, the sequence sizes and the running output offset computed per
-//     member in scalar registers (one v_readlane per member); a match the producer
-//     left unfinished (> 76 bytes) is extended by the whole wave.  Second half: the
-//     walked positions and match_end - 2 go into the table, the member records
-//     {literal start, output offset} to the emitter.
-//   EMITTER (wave 2), chunk s-3: every member lane writes its own sequence (token,
-//     literal length bytes, literals, offset, match length bytes) at its output
-//     offset; the last literals (:732-751) are copied with 16-byte moves.
+// The block is cut into chunks of 64 positions, one per lane.  The waves run in
+// lock step, two workgroup barriers per step s (each waits only on its own memory
+// operations; s_waitcnt vmcnt counts a wave's loads and stores together, in order):
+//   PRODUCER (wave 1), three chunks in flight:
+//     A(s+3)  load in[p, p+8) for every position p of the chunk;
+//     B(s+2)  hash in[p, p+5), read candidate T = table[h] (positions walked
+//             earlier plus match_end - 2, inserted as the reference does:
+//             :595-619, :680-706) and L = the earliest lane of the chunk with the
+//             same hash bits; copy the chunk into the ring; load in[T-4, T+28);
+//     C1(s+1) verify 4 bytes for T and L, measure both to 28 bytes forward and 4
+//             backward, keep the longer (then closer); load 32 more for a 28;
+//     C2(s)   (second half) finish those to 60 bytes, hash match_end - 2 ->
+//             match info of chunk s in LDS.
+//   WALKER (wave 0), chunk s-1: the greedy chain on the scalar unit (hops over the
+//     match lanes of a ballot mask), catch-up into pending literals (:623-627),
+//     the wave-wide extension of matches >= 60 bytes; second half: table inserts
+//     of the walked positions and match_end - 2 (:680), never overlapping B.
+//   EMITTER (wave 2), chunk s-2: sizes and prefix-sum offsets of the sequences,
+//     then each lane of a 64-byte output window computes its output byte; the
+//     last literals (:732-751) are copied with 16-byte moves.
 #include "lz4_gpu_internal.h"
 #include <stdlib.h>
 #include <type_traits>
@@ -47,8 +43,13 @@ namespace apelz4 {
 
 #ifdef APE_LZ4_STATS
 __device__ unsigned long long g_enc_stats[16];
+hipError_t enc_stats_v2_read(unsigned long long *out, int reset);
+// per-phase cycle sums of whichever encoder ran (the other one's are zero)
 hipError_t enc_stats_read(unsigned long long *out, int reset) {
+    unsigned long long v2[16];
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_enc_stats), sizeof(g_enc_stats));
+    if (e == hipSuccess) e = enc_stats_v2_read(v2, reset);
+    for (int i = 0; i < 16 && e == hipSuccess; i++) out[i] += v2[i];
     if (e == hipSuccess && reset) {
         unsigned long long z[16] = {0};
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_enc_stats), z, sizeof(z));
@@ -57,36 +58,49 @@ hipError_t enc_stats_read(unsigned long long *out, int reset) {
 }
 #endif
 
-hipError_t launch_encode_v1(const BlockArgs &a, hipStream_t s);
+hipError_t launch_encode_v2(const BlockArgs &a, hipStream_t s);
 
 namespace {
 
-constexpr int kHLog = 13;
+#ifndef APE_LZ4_HLOG
+#define APE_LZ4_HLOG 13
+#endif
+constexpr int kHLog = APE_LZ4_HLOG;
 constexpr int kHSize = 1 << kHLog;
-constexpr uint32_t kM1 = 12;   // stage 1 measures a match to this many bytes from p
-constexpr int kNI = 4;         // info / hash rings, in chunks (s-3 .. s)
-constexpr int kSmall = 128;    // smaller blocks take the byte-load path
+constexpr uint32_t kEagerLen = 28;   // match bytes measured by the producer (T candidate)
+constexpr uint32_t kEagerL = 12;     // ... for the in-chunk candidate L
+#ifndef APE_LZ4_ERING
+#define APE_LZ4_ERING 1024
+#endif
+constexpr uint32_t kRingE = APE_LZ4_ERING;  // recent input bytes (own, stage 2, end-2, literals)
+// Diagnostic A/B: with a 64 KiB ring the whole block window sits in LDS
+// and the candidate bytes (Y, E) are read from it instead of global memory -- 84 KiB
+// of LDS per block, one block per CU.  Never the product.
+constexpr bool kWin = kRingE >= 65536u;
+#ifndef APE_LZ4_SCRBITS
+#define APE_LZ4_SCRBITS 6
+#endif
+constexpr uint32_t kScr = 1u << APE_LZ4_SCRBITS;  // in-chunk candidate scratch entries
+constexpr int kSmall = 128;          // smaller blocks take the byte-load path
 
-// info.x: len (bits 0-15; bit 15 = TRUNC: measured to (len & 0x7FFF), longer) |
-//         back (16-18) | HAS (19) | HASHABLE (20)
-// info.y: offset (0-15) | hash (16-28)
-constexpr uint32_t X_TRUNC = 0x8000u, X_HAS = 1u << 19, X_HASHABLE = 1u << 20;
+
+// info.x: len (8) | back << 8 (3) | trunc << 11 | has << 12 | hashable << 13 |
+//         e2 << 14 | hash(match_end - 2) << 16;   info.y: offset | h << 16
+constexpr uint32_t I_TRUNC = 1u << 11, I_HAS = 1u << 12, I_HASHABLE = 1u << 13,
+                   I_E2 = 1u << 14;
 
 struct __attribute__((aligned(16))) EncLds {
-    uint16_t tab[kHSize];      // the reference's byU16 table (positions)
-    uint2 info[kNI][64];       // producer -> walker, emitter: chunk k at [k % 4]
-    uint16_t hr[kNI * 64];     // hash of position x at hr[x % 256] (walker: match_end - 2)
-    uint32_t scr[64];          // producer: earliest lane per low 6 hash bits
-    uint32_t sq[64];           // producer: stage-2 queue, owner lane | candidate << 8
-    uint32_t q[2][64];         // walker -> emitter: a batch of up to 64 sequences, member i
-                               // in lane i: {p | back << 16, len | offset << 16}
-    uint32_t qcnt;             // its count (0 = none pending; the emitter resets it)
-    uint2 wq[16];              // walker: one chunk's sequences (<= 16: matches are >= 4 long)
-    uint32_t xw[2][40];        // producer: chunk k's bytes in[64k-4, 64k+140) at [k % 2] (from
-                               // L(k) to M(k)): every lane's own window, the in-chunk
-                               // candidate and the stage-2 own segments (36 dwords + pad)
+    uint16_t tab[kHSize];
+    // input byte x at ring byte (x mod kRingE); the first 64 bytes are mirrored
+    // after the end, so a 36-byte read never wraps (immediate LDS offsets)
+    uint32_t ring[kRingE / 4 + 16];
+    uint2 info[3][64];               // producer -> walker and emitter, chunk k in [k % 3]
+    uint32_t scr[kScr];              // producer scratch: earliest lane per low hash bits
+    uint2 wres[2][64];               // walker -> emitter: {m_len | m_back << 20, anchor}
+    uint32_t wmem[2][2];             // walker -> emitter: member mask of the chunk
+    uint32_t wend;                   // walker -> emitter: final anchor (last literals)
+    uint32_t omap[16];               // emitter: owner map of a 64-byte output window
 };
-static_assert(sizeof(EncLds) <= 20480, "8 blocks per CU: 8 x 20 KiB = the 160 KiB LDS");
 
 // s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt at their maxima = no wait).  The
 // producer states its pipeline's waits explicitly: the compiler's own counter
@@ -104,8 +118,91 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// v_ffbl_b32 / v_ffbh_u32: lowest set bit / leading zeros, 0xFFFFFFFF for 0 (inline
-// asm so that the compiler does not turn the zero case into compare + select)
+// X = L shifted by d bytes (X byte i = L byte i + d, 0 outside L), |d| < 32,
+// with compile-time register indices only (a barrel shifter).
+__device__ __forceinline__ void shift_bytes(const uint32_t (&L)[8], int d, uint32_t (&X)[8]) {
+    uint32_t T[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) T[k] = L[k];
+    const bool down = d >= 0;
+    const int ad = down ? d : -d, w = ad >> 2;
+    const uint32_t r = (uint32_t)ad & 3u;
+#pragma unroll
+    for (int bit = 4; bit >= 1; bit >>= 1) {
+        if (w & bit) {
+            if (down) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) T[k] = (k + bit < 8) ? T[k + bit] : 0u;
+            } else {
+#pragma unroll
+                for (int k = 7; k >= 0; k--) T[k] = (k - bit >= 0) ? T[k - bit] : 0u;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (down) X[k] = __builtin_amdgcn_alignbyte(k + 1 < 8 ? T[k + 1] : 0u, T[k], r);
+        else X[k] = r ? __builtin_amdgcn_alignbyte(T[k], k >= 1 ? T[k - 1] : 0u, 4u - r) : T[k];
+    }
+}
+
+// 32 bytes in[pos, pos+32) (bytes outside [0, n) read as 0).
+// SMALL: byte loads.  Otherwise (n >= 32): two unaligned 16-byte loads from the
+// clamped window, fixed up with ALU only (so the wave's vmcnt accounting stays
+// static in the pipelined loop).
+// fast (wave-uniform): every lane's window is known to lie inside [0, n).
+template <bool SMALL>
+__device__ __forceinline__ void load32(gcu8 *in, int n, int pos, uint32_t (&X)[8],
+                                       bool fast = false) {
+    if (!SMALL && fast) {
+        gcu8 *q = in + (uint32_t)pos;   // saddr + voffset, +16 as the immediate offset
+        const uint4 a = gload16(q), b = gload16(q + 16);
+        X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w;
+        X[4] = b.x; X[5] = b.y; X[6] = b.z; X[7] = b.w;
+        return;
+    }
+    if (SMALL) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) X[k] = 0;
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+            const int q = pos + k;
+            if (q >= 0 && q < n) X[k >> 2] |= (uint32_t)in[(uint32_t)q] << (8 * (k & 3));
+        }
+        return;
+    }
+    const int ca = pos < 0 ? 0 : (pos > n - 32 ? n - 32 : pos);
+    gcu8 *q = in + (uint32_t)ca;
+    const uint4 a = gload16(q), b = gload16(q + 16);
+    const uint32_t L[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    if (ca == pos) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) X[k] = L[k];
+    } else {
+        // the clamped window ends at n / starts at 0, so shifting it zero-fills
+        // exactly the bytes outside [0, n)
+        const int d = pos - ca;   // |d| >= 32 only for lanes past the block end
+        shift_bytes(L, d < -31 ? -31 : (d > 31 ? 31 : d), X);
+        if (d > 31 || d < -31) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) X[k] = 0;
+        }
+    }
+}
+
+// Hash of the 5 bytes at p (x1 = in[p..p+3], b4 = in[p+4]) into kHLog bits.  The
+// reference multiplies the 40-bit sequence by 889523592379 (:456-473), which needs
+// quarter-rate 32-bit multiplies here; any hash gives a valid stream, so this one
+// uses two full-rate 24 x 24-bit multiplies (v_mul_u32_u24) of bytes 0-2 and
+// bytes 3-4.  Same ratio on the App. C data (tools/enc_model.c: 3.1613 vs 3.1600).
+__device__ __forceinline__ uint32_t hash5(uint32_t x1, uint32_t b4) {
+    const uint32_t lo = x1 & 0xFFFFFFu, hi = (x1 >> 24) | ((b4 & 0xFFu) << 8);
+    // (__umul24 returns int: do the sum and the shift unsigned)
+    return ((uint32_t)__umul24(lo, 0x9E3779u) + (uint32_t)__umul24(hi, 0xC2B2AEu)) >> (32 - kHLog);
+}
+
+// v_ffbl_b32 / v_ffbh_u32: lowest / highest set bit, 0xFFFFFFFF for 0 (inline asm
+// so that the compiler does not turn the zero case into compare + select)
 __device__ __forceinline__ uint32_t ffbl(uint32_t d) {
     uint32_t r;
     asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(d));
@@ -117,28 +214,40 @@ __device__ __forceinline__ uint32_t ffbh(uint32_t d) {
     return r;
 }
 
-// Hash of the 5 bytes at p (x1 = in[p..p+3], b4 = in[p+4]) into kHLog bits.  The
-// reference multiplies the 40-bit sequence by 889523592379 (:456-473), which needs
-// quarter-rate 32-bit multiplies here; any hash gives a valid stream, so this one
-// uses two 24 x 24-bit multiplies (v_mul_u32_u24) of bytes 0-2 and bytes 3-4.
-// Same ratio on the App. C data (tools/enc_model.c: 3.1613 vs 3.1600).
-__device__ __forceinline__ uint32_t hash5(uint32_t x1, uint32_t b4) {
-    const uint32_t lo = x1 & 0xFFFFFFu, hi = (x1 >> 24) | ((b4 & 0xFFu) << 8);
-    return ((uint32_t)__umul24(lo, 0x9E3779u) + (uint32_t)__umul24(hi, 0xC2B2AEu)) >> (32 - kHLog);
+// first differing bit of dwords A[K0..K1) vs B (bit index from A[K0]'s bit 0), or
+// 0xFFFFFFFF: ffbl + saturating add + min3 per dword, no compares or selects
+template <int K0, int K1>
+__device__ __forceinline__ uint32_t first_diff_bit(const uint32_t (&A)[8], const uint32_t (&B)[8]) {
+    uint32_t m = ffbl(A[K0] ^ B[K0]);
+#pragma unroll
+    for (int k = K0 + 1; k < K1; k++)
+        m = umin(m, __builtin_elementwise_add_sat(ffbl(A[k] ^ B[k]), 32u * (uint32_t)(k - K0)));
+    return m;
 }
 
-// e / 255 with one 24-bit multiply: 255 * 0x8081 = 2^23 + 127, so
+// common length of X and Y from byte 4 (dword 1) on, up to kEagerLen
+__device__ __forceinline__ uint32_t eager(const uint32_t (&X)[8], const uint32_t (&Y)[8]) {
+    return umin((first_diff_bit<2, 8>(X, Y) >> 3) + 4u, kEagerLen);
+}
+
+// bytes equal just before the match (in[p-1] == in[c-1], ...), 0..4
+__device__ __forceinline__ uint32_t back4(uint32_t x0, uint32_t y0) {
+    return umin(ffbh(x0 ^ y0) >> 3, 4u);
+}
+
+// e / 255 with one full-rate 24-bit multiply: 255 * 0x8081 = 2^23 + 127, so
 // floor(e * 0x8081 / 2^23) = floor(e / 255) for e < 66060 (lengths here are < 65537)
 __device__ __forceinline__ uint32_t div255(uint32_t e) {
     return (uint32_t)__umul24(e, 0x8081u) >> 23;
 }
-// bytes after a 15 nibble: v < 15 -> 0, else (v - 15) / 255 + 1 = (v + 240) / 255
-__device__ __forceinline__ uint32_t ext_bytes(uint32_t v) { return div255(v + 240u); }
-__host__ __device__ __forceinline__ uint32_t ext_s(uint32_t v) {   // scalar form
-    return ((v + 240u) * 0x8081u) >> 23;
+
+// bytes after a 15 nibble: v < 15 -> 0, else (v - 15) / 255 + 1 -- both are
+// (v + 240) / 255 (v + 240 < 255 below 15; one full-rate multiply, no select)
+__device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {
+    return div255(v + 240u);
 }
 
-// write the length extension of v (>= 15) at o, at most `room` bytes (never past cap)
+// write the length extension of v (>= 15) at o
 __device__ __forceinline__ void put_len(gu8 *o, uint32_t v) {
     if (v < 15) return;
     v -= 15;
@@ -147,68 +256,21 @@ __device__ __forceinline__ void put_len(gu8 *o, uint32_t v) {
     o[k] = (uint8_t)v;
 }
 
-// X = L shifted by d bytes (X byte i = L byte i + d, 0 outside L), |d| < 16, with
-// compile-time register indices only.
-__device__ __forceinline__ void shift16(const uint32_t (&L)[4], int d, uint32_t (&X)[4]) {
-    uint32_t T[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) T[k] = L[k];
-    const bool down = d >= 0;
-    const int ad = down ? d : -d, w = ad >> 2;
-    const uint32_t r = (uint32_t)ad & 3u;
-#pragma unroll
-    for (int bit = 2; bit >= 1; bit >>= 1) {
-        if (w & bit) {
-            if (down) {
-#pragma unroll
-                for (int k = 0; k < 4; k++) T[k] = (k + bit < 4) ? T[k + bit] : 0u;
-            } else {
-#pragma unroll
-                for (int k = 3; k >= 0; k--) T[k] = (k - bit >= 0) ? T[k - bit] : 0u;
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        if (down) X[k] = __builtin_amdgcn_alignbyte(k + 1 < 4 ? T[k + 1] : 0u, T[k], r);
-        else X[k] = r ? __builtin_amdgcn_alignbyte(T[k], k >= 1 ? T[k - 1] : 0u, 4u - r) : T[k];
-    }
+// 4 input bytes at x from the ring
+__device__ __forceinline__ uint32_t ring4(const EncLds &S, uint32_t x) {
+    const uint32_t *r = S.ring + ((x >> 2) & (kRingE / 4 - 1));
+    return __builtin_amdgcn_alignbyte(r[1], r[0], x & 3u);
 }
 
-// 16 bytes in[pos, pos+16) (bytes outside [0, n) read as 0).  fast (wave-uniform): every
-// lane's window lies inside [0, n).  SMALL: byte loads.  Otherwise (n >= 16) one
-// unaligned 16-byte load from the clamped window, fixed up with ALU only.
-template <bool SMALL>
-__device__ __forceinline__ void load16(gcu8 *in, int n, int pos, uint32_t (&X)[4], bool fast) {
-    if (!SMALL && fast) {
-        const uint4 a = gload16(in + (uint32_t)pos);
-        X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w;
-        return;
-    }
-    if (SMALL) {
+// 32 input bytes at x from the ring
+__device__ __forceinline__ void ring32(const EncLds &S, uint32_t x, uint32_t (&O)[8]) {
+    const uint32_t *r = S.ring + ((x >> 2) & (kRingE / 4 - 1));
+    const uint32_t sh = x & 3u;
+    uint32_t W[9];
 #pragma unroll
-        for (int k = 0; k < 4; k++) X[k] = 0;
+    for (int k = 0; k < 9; k++) W[k] = r[k];
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int q = pos + k;
-            if (q >= 0 && q < n) X[k >> 2] |= (uint32_t)in[(uint32_t)q] << (8 * (k & 3));
-        }
-        return;
-    }
-    const int ca = pos < 0 ? 0 : (pos > n - 16 ? n - 16 : pos);
-    const uint4 a = gload16(in + (uint32_t)ca);
-    const uint32_t L[4] = {a.x, a.y, a.z, a.w};
-    const int d = pos - ca;
-    if (d == 0) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) X[k] = L[k];
-    } else {
-        shift16(L, d < -15 ? -15 : (d > 15 ? 15 : d), X);
-        if (d > 15 || d < -15) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) X[k] = 0;
-        }
-    }
+    for (int k = 0; k < 8; k++) O[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
 }
 
 // Copy in[a, a+len) to dst[o, o+len) with the whole wave (16 bytes per lane per step).
@@ -233,190 +295,174 @@ struct Blk {
                                      // history prefix (withPrefix encode), only hashed
     uint32_t nr;                     // bytes to encode (n - 64 k0)
     bool noL;                        // acceleration > 1: no in-chunk candidate
+    uint32_t stride;                 // acceleration: search every stride-th position
+    uint64_t pat;                    // bits 0, stride, 2 stride, ... (< 64)
 };
 
 // ---------------- producer ----------------
-// Per chunk in flight (the step loop is unrolled by two, so no register set is ever
-// copied): own bytes X of the chunk H and M work on; candidates and hash from H.
-// Set k % 2 holds chunk k's own bytes X (L(k) .. M(k)), candidates, hash and their
-// bytes Y / Z (H(k) .. M(k)), and the stage-2 bytes (M(k) .. F(k)); the two chunks
-// in flight with one parity never overlap in the fields they use.
-struct PSet {
-    uint32_t X[4];                   // own bytes [p-4, p+12)
-    uint32_t cT, cL, h;              // candidates (~0 = none), hash
-    uint32_t Y[4], Z[4];             // T / L candidate bytes [c-4, c+12)
-    uint32_t A[4], Bc[4];            // stage-2 bytes: own / candidate segment
-    uint32_t q2;                     // stage-2 owner lane | seg << 8, ~0 = idle lane
-    uint32_t lg;                     // stage-2 lanes per candidate, log2 (wave-uniform)
+struct Part {                        // C1 result of one chunk, finished by C2
+    uint32_t len, c, bk, lim, h, base;   // base: bytes C1 measured (kEagerLen / kEagerL)
+    bool has, hashable, trunc1;
 };
 
-// L(k): the chunk's 144 bytes in[64k-4, 64k+140), one dword per lane 0..35 (bytes
-// outside [0, n) read as 0) -- through the texture path once instead of as 64
-// overlapping 16-byte windows plus the stage-2 own segments; x_spread makes the
-// windows.  Outside SMALL one load instruction.
-template <bool SMALL, bool FAST>
-__device__ __forceinline__ void p_load(const Blk &B, int k, int lane, uint32_t &xd) {
-    // lanes 36..63 repeat lane 35's address (no branch: the compiler's wait-count
-    // model would take a skippable load as not issued and wait for older loads)
-    const int w = (k < B.nch ? 64 * k : 0) - 4 + 4 * (lane < 36 ? lane : 35);
-    if (SMALL) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-            if (w + t >= 0 && w + t < B.n) v |= (uint32_t)B.in[(uint32_t)(w + t)] << (8 * t);
-        xd = v;
-    } else if (FAST) {
-        xd = gload4(B.in + (uint32_t)w);
-    } else {   // clamped into [0, n - 4] (n >= 128 here), then shifted into place
-        const int a = w < 0 ? 0 : (w > B.n - 4 ? B.n - 4 : w);
-        const uint32_t v = gload4(B.in + (uint32_t)a);
-        const int d = w - a;   // -4 .. 4
-        const uint32_t dn = d > 0 ? (d < 4 ? v >> (8 * d) : 0u) : 0u;
-        const uint32_t up = d < 0 ? (d > -4 ? v << (-8 * d) : 0u) : 0u;
-        xd = d == 0 ? v : (d > 0 ? dn : up);
+// One parity of the producer pipeline (the step loop is unrolled by two, so no
+// register set is ever copied): X from A for B, Y/cT/jL/h from B for C1, q/E from
+// C1 for C2.
+struct PSet {
+    uint32_t X[2];                   // own bytes in[p, p+8) of the chunk B works on next
+    uint32_t Y[8];                   // T-candidate bytes
+    uint32_t E[8];                   // second-stage candidate bytes
+    uint32_t cT, jL, h;
+    Part q;
+};
+
+// A(k): own bytes in[p, p+8) for the hash (0 past the block end)
+template <bool SMALL, bool FAST = false>
+__device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_t (&X)[2]) {
+    const uint32_t pos = (k < B.nch ? 64u * (uint32_t)k : 0u) + (uint32_t)lane;
+    if (FAST || (!SMALL && 64 * k + 72 <= B.n)) {   // wave-uniform: the whole window is inside
+        const uint2 v = gload8(B.in + pos);
+        X[0] = v.x;
+        X[1] = v.y;
+        return;
     }
+    X[0] = X[1] = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < 8u; t++)
+        if (pos + t < B.un) X[t >> 2] |= (uint32_t)B.in[pos + t] << (8 * (t & 3));
 }
 
-// 16 bytes at byte offset j (0..128) of a chunk image: five dwords, four alignbytes
-__device__ __forceinline__ void x_window(const uint32_t *img, uint32_t j, uint32_t (&X)[4]) {
-    const uint32_t *w = img + (j >> 2);
-    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
-    const uint32_t r = j & 3u;
-    X[0] = __builtin_amdgcn_alignbyte(w1, w0, r);
-    X[1] = __builtin_amdgcn_alignbyte(w2, w1, r);
-    X[2] = __builtin_amdgcn_alignbyte(w3, w2, r);
-    X[3] = __builtin_amdgcn_alignbyte(w4, w3, r);
+// T candidate bytes of chunk k (issued one step before C1 consumes them).  Candidates
+// below position 4 are skipped: their 4 bytes of backward context would start before
+// the block and need the slow edge path (never-written slots read as 0).
+template <bool SMALL, bool FAST = false>
+__device__ __forceinline__ void prod_fetch_t(const Blk &B, int k, int lane, uint32_t cT,
+                                             uint32_t (&Y)[8]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const bool tryT = k < B.nch && cT < p && cT >= 4u;
+    load32<SMALL>(B.in, B.n, tryT ? (int)cT - 4 : 0, Y, FAST || 64 * k + 91 <= B.n);
 }
 
-// the loaded dwords of chunk k -> its LDS image -> every lane's own window in[p-4, p+12)
-__device__ __forceinline__ void x_spread(EncLds &S, int k, int lane, uint32_t xd, uint32_t (&X)[4]) {
-    uint32_t *img = S.xw[k & 1];
-    if (lane < 36) img[lane] = xd;
-    wave_sync();
-    x_window(img, (uint32_t)lane, X);
-}
-
-// H(k): hash, table + in-chunk candidates, hash ring, candidate loads
-template <bool SMALL, bool FAST>
-__device__ __forceinline__ void p_lookup(EncLds &S, const Blk &B, int k, int lane, PSet &C) {
-    const uint32_t (&X)[4] = C.X;
+// B(k): hash, table + in-chunk candidates, T fetch issue, ring copy
+template <bool SMALL, bool FAST = false>
+__device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int lane,
+                                            const uint32_t (&X)[2], uint32_t &cT, uint32_t &jL,
+                                            uint32_t &h, uint32_t (&Y)[8]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const bool live = k < B.nch;
     const bool hashable = live && p + 5u <= B.un;
-    const uint32_t h = hash5(X[1], X[2]);
-    const uint32_t cT = S.tab[h];
-    S.hr[p & (kNI * 64 - 1)] = (uint16_t)h;
-    uint32_t jL = 0xFFFFFFFFu;
+    h = hash5(X[0], X[1]);
+    cT = S.tab[h];
+    jL = 0xFFFFFFFFu;
     if (!B.noL) {   // wave-uniform
-        const uint32_t hs = h & 63u;
+        const uint32_t hs = h & (kScr - 1u);
         if (hashable) atomicMin(&S.scr[hs], (uint32_t)lane);
         wave_sync();
         jL = hashable ? S.scr[hs] : 0xFFFFFFFFu;
         wave_sync();
         if (hashable) S.scr[hs] = 0xFFFFFFFFu;
     }
-    // Candidates below position 4 are skipped: their 4 bytes of backward context would
-    // start before the block (and a candidate is always < p <= n - 12, so its 16 bytes
-    // lie inside the block).
-    // only positions that may start a match (p <= n - 12, :585) keep candidates, so a
-    // candidate c < p has its 16 bytes [c - 4, c + 12) inside the block
-    const bool can = hashable && p >= 1u && p <= B.mstart && B.n >= kMinLength;
-    const uint32_t cL = 64u * (uint32_t)k + jL;
-    const bool okT = can && cT < p && cT >= 4u;
-    const bool okL = can && jL < (uint32_t)lane && cL >= 4u && cL != cT;
-    C.h = h;
-    C.cT = okT ? cT : 0xFFFFFFFFu;
-    C.cL = okL ? cL : 0xFFFFFFFFu;
-    // dummy loads of idle lanes read the block start (n >= 16 outside SMALL); the
-    // in-chunk candidate's bytes come from the chunk image in M
-    load16<SMALL>(B.in, B.n, okT ? (int)cT - 4 : 0, C.Y, !SMALL);
-}
-
-// first differing byte of A vs B over 4 dwords (0..15), 0x1FFFFFFF if all 16 equal:
-// ffbl per dword, the dword's bit offset ORed in (a full-rate or instead of an add),
-// then a min over the four
-__device__ __forceinline__ uint32_t first_diff16(const uint32_t (&A)[4], const uint32_t (&B)[4]) {
-    const uint32_t m0 = ffbl(A[0] ^ B[0]), m1 = ffbl(A[1] ^ B[1]) | 32u;
-    const uint32_t m2 = ffbl(A[2] ^ B[2]) | 64u, m3 = ffbl(A[3] ^ B[3]) | 96u;
-    return umin(umin(m0, m1), umin(m2, m3)) >> 3;
-}
-
-// M(k): verify + measure both candidates to 12 bytes, back-extension, pick -> info;
-// queue the saturated lanes and issue their stage-2 loads.
-template <bool SMALL, bool FAST>
-__device__ __forceinline__ void p_measure(EncLds &S, const Blk &B, int k, int lane, PSet &C) {
-    const uint32_t (&X)[4] = C.X;
-    const PSet &Sh = C;
-    // in-chunk candidate bytes [cL-4, cL+12) = image bytes [cL - 64k, +16)
-    x_window(S.xw[k & 1], C.cL != 0xFFFFFFFFu ? C.cL & 63u : 0u, C.Z);
-    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-    const bool live = k < B.nch;
-    const bool can = live && p >= 1u && p <= B.mstart && B.n >= kMinLength;
-    const uint32_t lim = can ? B.mlimit - p : 0u;
-    // bytes 4..11 from p: dwords 2, 3 of the own / candidate windows (window = c - 4)
-    const bool vT = can && C.cT != 0xFFFFFFFFu && Sh.Y[1] == X[1];
-    const bool vL = can && C.cL != 0xFFFFFFFFu && Sh.Z[1] == X[1];
-    const uint32_t bT = umin(umin(ffbl(X[2] ^ Sh.Y[2]), ffbl(X[3] ^ Sh.Y[3]) | 32u) >> 3, 8u);
-    const uint32_t bL = umin(umin(ffbl(X[2] ^ Sh.Z[2]), ffbl(X[3] ^ Sh.Z[3]) | 32u) >> 3, 8u);
-    // L (the closer one) wins when longer, or equally long below 12
-    const bool pickL = vL && (!vT || bL > bT || (bL == bT && bT < 8u));
-    const uint32_t c = pickL ? C.cL : C.cT;
-    const bool has = vT || vL;
-    uint32_t len = 4u + (pickL ? bL : bT);
-    const uint32_t w0 = pickL ? Sh.Z[0] : Sh.Y[0];
-    const uint32_t back = umin(ffbh(X[0] ^ w0) >> 3, 4u);   // in[p-1..p-4] == in[c-1..c-4]
-    len = umin(len, lim);
-    const bool sat = has && len == kM1 && lim > kM1;
-    const bool hashable = live && p + 5u <= B.un;
-    S.info[k % kNI][lane] =
-        make_uint2((has ? len : 0u) | (back << 16) | (has ? X_HAS : 0u) | (hashable ? X_HASHABLE : 0u),
-                   (has ? p - c : 0u) | (C.h << 16));
-    // ---- stage 2: compact the saturated lanes, 64 / nsat lanes (4, 2 or 1) each ----
-    const uint64_t sm = wave_ballot(sat);
-    const uint32_t nsat = (uint32_t)__popcll(sm);
-    const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-    if (sat) S.sq[idx] = (uint32_t)lane | (c << 8);
-    wave_sync();
-    const uint32_t lg = nsat <= 16u ? 2u : (nsat <= 32u ? 1u : 0u);
-    const uint32_t slot = (uint32_t)lane >> lg, seg = (uint32_t)lane & ((1u << lg) - 1u);
-    const bool act = slot < nsat;
-    const uint32_t e = S.sq[act ? slot : 0u];
-    const uint32_t j = e & 63u, cc = e >> 8;
-    const uint32_t P = 64u * (uint32_t)k;
-    C.q2 = act ? (j | (seg << 8)) : 0xFFFFFFFFu;
-    C.lg = lg;
-    // own segment p_j + 12 + 16 seg from the chunk image (byte j + 16 + 16 seg <= 127),
-    // candidate segment c + 12 + 16 seg (16 bytes each); idle lanes load the block start
-    x_window(S.xw[k & 1], act ? j + kM1 + 4u + 16u * seg : 0u, C.A);
-    (void)P;
-    const int pc = act ? (int)(cc + kM1 + 16u * seg) : 0;
-    load16<SMALL>(B.in, B.n, pc, C.Bc, FAST);
-}
-
-// F(k): finish the saturated lengths of chunk k (loads issued one step earlier)
-__device__ __forceinline__ void p_finish(EncLds &S, const Blk &B, int k, int lane, const PSet &Sh) {
-    const uint32_t lg = __builtin_amdgcn_readfirstlane(Sh.lg);
-    if (k < 0) return;
-    uint32_t v = umin(first_diff16(Sh.A, Sh.Bc) + 16u * ((Sh.q2 >> 8) & 3u), 0xFFFFu);
-    // minimum over the 1 << lg lanes of a candidate (quad_perm swaps), to its first lane
-    if (lg >= 1u) v = umin(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false));
-    if (lg >= 2u) v = umin(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false));
-    const uint32_t span = 16u << lg;
-    if (Sh.q2 < 64u) {   // the candidate's first lane (seg 0)
-        const uint32_t j = Sh.q2;
-        const uint32_t lim = B.mlimit - (64u * (uint32_t)k + j);
-        const bool full = v >= 0xFFFFu;                  // equal over the whole span
-        uint32_t len = kM1 + (full ? span : v);
-        const bool trunc = full && lim > kM1 + span;
-        len = umin(len, lim);
-        *(uint16_t *)&S.info[k % kNI][j].x = (uint16_t)(len | (trunc ? X_TRUNC : 0u));
+    // ring copy of this chunk (own bytes for C1, second stage, match_end - 2,
+    // literals); zero past the block end
+    if (live) {
+        const uint8_t by = (uint8_t)X[0];
+        ((uint8_t *)S.ring)[p & (kRingE - 1)] = by;
+        if (((64u * (uint32_t)k) & (kRingE - 1)) == 0u) ((uint8_t *)S.ring)[kRingE + lane] = by;
     }
+    // T candidate bytes (issued now, consumed one step later).  Candidates below
+    // position 4 are skipped: their 4 bytes of backward context would start before
+    // the block and need the slow edge path (never-written slots read as 0).
+    if (!kWin) prod_fetch_t<SMALL, FAST>(B, k, lane, cT, Y);
+}
+
+// C1(k): verify / measure 28 bytes / pick; issue the second-stage load
+template <bool SMALL, bool FAST = false>
+__device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int k, int lane,
+                                             const uint32_t (&Y)[8], uint32_t cT, uint32_t jL,
+                                             uint32_t h, Part &R, uint32_t (&E)[8]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    uint32_t X[8];
+    ring32(S, p - 4u, X);            // own bytes in[p-4, p+28) (ring tail = 0 before 0)
+    uint32_t Yw[8];
+    if (kWin) {   // candidate bytes from the LDS window (chunks <= k+1 are in it by now)
+        const bool tryT = k < B.nch && cT < p && cT >= 4u;
+        ring32(S, tryT ? cT - 4u : 0u, Yw);
+    }
+    const uint32_t (&Yr)[8] = kWin ? Yw : Y;
+#define Y Yr
+    const bool live = k < B.nch;
+    R.hashable = live && p + 5u <= B.un;
+    const bool can = live && p >= 1u && p <= B.mstart && B.n >= kMinLength;
+    const uint32_t cL = 64u * (uint32_t)k + jL;
+    // L candidate bytes in[cL-4, cL+12) from lane jL's own bytes
+    uint32_t Z[8];
+#pragma unroll
+    for (int t = 0; t < 4; t++) Z[t] = (uint32_t)__shfl((int)X[t], (int)(jL & 63u), 64);
+#pragma unroll
+    for (int t = 4; t < 8; t++) Z[t] = 0u;
+    const bool okT = can && cT < p && cT >= 4u && Y[1] == X[1];
+    const bool okL = can && jL < (uint32_t)lane && cL != cT && Z[1] == X[1];   // jL = ~0 if noL
+    R.lim = can ? B.mlimit - p : 0u;
+    // measured unconditionally (selects, no branches): every lane reads Y, so the
+    // compiler sees the candidate load consumed on every path.  T to 28 bytes, L to 12:
+    // L (the closer one) is taken when T is shorter than 12 and L at least as long,
+    // and C2 continues the taken candidate from where C1 stopped
+    // (tools/enc_model.c model4, pol 7 vs 0: ratio -0.1 %; measured -0.06 %, -3.4 % VALU).
+    const uint32_t eT = eager(X, Y);
+    const uint32_t eL = umin((first_diff_bit<2, 4>(X, Z) >> 3) + 4u, kEagerL);
+    const uint32_t lT = okT ? eT : 0u, lL = okL ? eL : 0u;
+    const bool pickL = okL && (!okT || (lT < kEagerL && lL >= lT));
+    R.c = pickL ? cL : cT;
+    R.len = pickL ? lL : lT;
+    R.base = pickL ? kEagerL : kEagerLen;
+    R.trunc1 = R.len >= R.base && R.lim > R.base;
+    if (R.len > R.lim) R.len = R.lim;
+    R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
+    R.has = okT || okL;
+    R.h = h;
+#undef Y
+    if (kWin) {
+        ring32(S, R.trunc1 ? R.c + R.base : 0u, E);
+        return;
+    }
+    load32<SMALL>(B.in, B.n, R.trunc1 ? (int)(R.c + R.base) : 0, E,
+                  FAST || 64 * k + 123 <= B.n);
+}
+
+// C2(k): finish the truncated lengths against the ring, hash match_end - 2 -> info
+__device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int lane,
+                                            const Part &R, const uint32_t (&E)[8]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    uint32_t len = R.len;
+    bool trunc = false;
+    {   // unconditional for the same reason as in C1
+        uint32_t O[8];
+        ring32(S, p + R.base, O);                // own bytes p+base .. p+base+32
+        const uint32_t ext = umin(first_diff_bit<0, 8>(O, E) >> 3, 32u);
+        if (R.trunc1) {
+            len = umin(R.base + ext, R.lim);
+            trunc = ext == 32u && R.lim > R.base + 32u;
+        }
+    }
+    uint32_t e2 = 0;
+    if (R.has && !trunc) {
+        const uint32_t at = p + len - 2u;         // match end - 2 (:680)
+        if (at + 5u <= B.un) e2 = I_E2 | (hash5(ring4(S, at), ring4(S, at + 4u)) << 16);
+    }
+    S.info[k % 3][lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
+                                         (R.has ? I_HAS : 0u) | (R.hashable ? I_HASHABLE : 0u) | e2,
+                                     (R.has ? p - R.c : 0u) | (R.h << 16));
 }
 
 // ---------------- walker ----------------
-// forward extension of the match at m (candidate cm) from L bytes on, with the whole
-// wave, 1 KiB per step; returns the full length (<= mlimit - m)
+struct Walk {
+    uint32_t q;          // walk position (the next probe)
+    uint32_t anchor;     // start of the pending literals
+    uint32_t dense;      // acceleration: consecutive probes left before the stride phase
+};
+
+// forward extension of the match at m (candidate cm) from L bytes on, with the
+// whole wave, 1 KiB per step; returns the full length (<= mlimit - m)
 __device__ __forceinline__ uint32_t extend_match(const Blk &B, uint32_t m, uint32_t cm, uint32_t L,
                                                  int lane) {
     const uint32_t lm = B.mlimit - m;
@@ -456,214 +502,246 @@ __device__ __forceinline__ uint32_t extend_match(const Blk &B, uint32_t m, uint3
     return L > lm ? lm : L;
 }
 
-struct Walk {
-    uint32_t q;          // walk position (next position to search)
-    uint32_t a;          // anchor: start of the pending literals
-    uint32_t qn;         // sequences in the queue registers
-    uint32_t Q0, Q1;     // per lane: queued sequence {p | back << 16, len | offset << 16}
-    uint32_t nx;         // (diagnostic) walker extensions
-};
+// Walk chunk k (first half of step k + 1), then (second half) insert the walked
+// positions and match_end - 2 into the table and hand the members to the emitter.
+// The greedy chain (:591-627: a position with a match jumps past it, any other
+// position is a literal): the scalar unit hops over the match lanes only (ballot
+// mask, one v_readlane per member); walked positions, catch-up limits (:623-627)
+// and the new anchor follow for all 64 lanes at once from the member set.  A match
+// the producer could not finish (TRUNC, >= 60 bytes) is extended by the whole wave.
 struct WalkOut {
-    bool walked;         // this lane's position was walked (table insert)
-    bool member;         // a match starts here
-    uint32_t x, y;       // info of the lane (final lengths)
-    uint64_t M;          // match starts of the chunk
-    uint32_t rel0;       // first position the walk searched (64: none)
+    uint64_t walked, members;
+    uint32_t m_back, m_len, an;   // per member lane
+    uint2 iv;
+    uint32_t q0, Lf;              // walk start; forward match length per lane
 };
 
-// hand the queued sequences to the emitter (it consumes them in the next step)
-__device__ __forceinline__ void walk_flush(EncLds &S, int lane, Walk &W) {
-    S.q[0][lane] = W.Q0;
-    S.q[1][lane] = W.Q1;
-    if (lane == 0) S.qcnt = W.qn;
-    W.qn = 0;
-}
-
-// per-lane bit of a wave-uniform 64-bit mask: v_cndmask with the mask as the condition
-__device__ __forceinline__ bool lane_bit(uint64_t m) {
-    uint32_t r;
-    asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(r) : "s"(m));
-    return r != 0u;
-}
-
-// First half: the greedy chain (:591-627) over chunk k.  Only the chain itself runs on
-// the scalar unit -- next match start, one v_readlane of its length, jump past it; the
-// rest follows lane-parallel from the member set: one max-scan of the members' ends
-// gives every member its catch-up limit (<= 4 bytes back, never into the previous
-// match, :623-627) and every lane whether a match covers it; the members' sequences
-// then move to the next free lanes of the queue registers through a small LDS buffer,
-// so the emitter later writes 64 sequences per pass.
-__device__ __forceinline__ void walk_chain(const Blk &B, int k, int lane, Walk &W, WalkOut &O,
-                                           const uint2 iv) {
+// First half: the hop chain only (the latency-bound part); second half, before the
+// inserts: the lane-parallel catch-up limits, walked set and anchor (walk_finish).
+template <bool ACC>
+__device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k, int lane, Walk &W,
+                                           WalkOut &O) {
     const uint32_t P = 64u * (uint32_t)k;
-    O.x = iv.x;
-    O.y = iv.y;
-    O.walked = O.member = false;
-    O.M = 0;
-    O.rel0 = 64u;
-    if (W.q >= P + 64u) return;               // a match from an earlier chunk covers it
-    const uint64_t Hm = wave_ballot((iv.x & X_HAS) != 0u);
-    const uint32_t rel0 = W.q - P;
-    uint32_t rel = rel0;
+    O.walked = O.members = 0;
+    O.m_back = O.m_len = O.an = 0;
+    O.iv = S.info[k % 3][lane];
+    O.q0 = W.q;
+    O.Lf = O.iv.x & 0xFFu;                               // forward match length
+    if (W.q >= P + 64u) return;               // a match from earlier chunks covers it
+    const uint2 iv = O.iv;
+    const bool has = (iv.x & I_HAS) != 0u, trunc = (iv.x & I_TRUNC) != 0u;
+    const uint64_t Hm = wave_ballot(has);
+    const uint32_t Lh = has ? (trunc ? 0x80u : O.Lf) : 0u;   // hop; 0x80 = unfinished
+    uint32_t rel = W.q - P;
     uint64_t M = 0;
     for (;;) {
-        const uint64_t w = Hm >> rel;
-        if (w == 0) { rel = 64u; break; }
-        const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
-        uint32_t len = lane_val(O.x, (int)j) & 0xFFFFu;
-        if (len & X_TRUNC) {                  // unfinished by the producer (rare)
-            W.nx++;
-            const uint32_t m = P + j;
-            len = extend_match(B, m, m - (lane_val(O.y, (int)j) & 0xFFFFu), len & 0x7FFFu, lane);
-            if ((uint32_t)lane == j) O.x = (O.x & 0xFFFF0000u) | len;
+        // acceleration (:591-600): after a match end e the reference tests e (:710-720),
+        // then searches from e+1 with step 1 once and then step = acceleration (without
+        // the growth after 64 misses): probes e, e+1, e+2, e+2+a, e+2+2a, ...  `dense`
+        // = consecutive probes left from rel; then every stride-th.
+        const uint32_t dn = W.dense;
+        const uint64_t pm = !ACC ? ~0ull
+                                 : (dn ? ((1ull << dn) - 1ull) | (B.pat << (dn - 1u)) : B.pat);
+        const uint64_t w = (Hm >> rel) & pm;
+        if (w == 0) {   // next probe position past the chunk
+            if (!ACC) {
+                rel = 64u;
+            } else if (rel + dn > 64u) {          // still in the consecutive probes
+                W.dense = rel + dn - 64u;
+                rel = 64u;
+            } else {
+                const uint32_t b = dn ? rel + dn - 1u : rel;   // the stride phase's base
+                rel = b + ((64u - b + B.stride - 1u) / B.stride) * B.stride;
+                W.dense = 0;
+            }
+            break;
         }
+        const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
+        const uint32_t h = lane_val(Lh, (int)j);
         M |= 1ull << j;
-        rel = j + len;
+        if (h & 0x80u) {
+            const uint32_t me = P + j;
+            const uint32_t cm = me - (lane_val(iv.y, (int)j) & 0xFFFFu);
+            const uint32_t Le = extend_match(B, me, cm, lane_val(iv.x, (int)j) & 0xFFu, lane);
+            if ((uint32_t)lane == j) O.Lf = Le;
+            rel = j + Le;
+        } else {
+            rel = j + h;
+        }
+        if (ACC) W.dense = 3u;   // a new search from the match end
         if (rel >= 64u) break;
     }
+    O.members = M;
     W.q = P + rel;
-    O.M = M;
-    O.rel0 = rel0;
 }
 
-// Second half, before the inserts: the member set's lane-parallel consequences.
-__device__ __forceinline__ void walk_post(EncLds &S, int k, int lane, Walk &W, WalkOut &O) {
+template <bool ACC>
+__device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk &W, WalkOut &O) {
     const uint32_t P = 64u * (uint32_t)k;
-    if (O.rel0 >= 64u) return;
-    const uint64_t M = O.M;
+    if (O.q0 >= P + 64u) return;              // covered by a match from earlier chunks
+    // catch-up limits: a member's backward extension stops at the previous end
+    const uint32_t anchor0 = W.anchor;
+    const bool mem = (O.members >> lane) & 1ull;
     const uint32_t p = P + (uint32_t)lane;
-    const bool mem = lane_bit(M);
-    const uint32_t len = O.x & 0xFFFFu;
-    const uint32_t im = wave_incl_max(mem ? p + len : 0u);   // latest match end up to here
-    const uint32_t prev = umax(wave_shr1(im, 0u), W.a);      // ... before this lane
-    O.member = mem;
-    O.walked = (uint32_t)lane >= O.rel0 && prev <= p;         // not inside a match
-    W.a = umax(W.a, lane_val(im, 63));
-    if (!M) return;
-    // the members' sequences, in order, to queue lanes qn, qn + 1, ...
-    const uint32_t back = umin((O.x >> 16) & 7u, p - prev);
-    const uint32_t nm = (uint32_t)__popcll(M);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
-    if (mem) S.wq[rank] = make_uint2(p | (back << 16), len | (O.y << 16));
-    wave_sync();
-    const uint32_t d = (uint32_t)lane - W.qn;                // lanes qn .. qn + nm - 1
-    const uint2 e = S.wq[d < nm ? d : 0u];
-    if (d < nm) { W.Q0 = e.x; W.Q1 = e.y; }
-    if (W.qn + nm >= 64u) {                                   // a full batch: hand it over
-        const uint32_t done = 64u - W.qn;                     // members that fit it
-        W.qn = 64u;
-        walk_flush(S, lane, W);
-        const uint32_t rest = nm - done;                      // the others start the next
-        const uint2 f = S.wq[(uint32_t)lane < rest ? done + (uint32_t)lane : 0u];
-        if ((uint32_t)lane < rest) { W.Q0 = f.x; W.Q1 = f.y; }
-        W.qn = rest;
-    } else {
-        W.qn += nm;
-    }
+    const uint32_t end = mem ? p + O.Lf : 0u;
+    const uint32_t imax = wave_incl_max(end);
+    const uint32_t pm = umax(wave_shr1(imax, 0u), anchor0);
+    const uint32_t bk = umin((O.iv.x >> 8) & 7u, p - pm);
+    O.m_back = bk;
+    O.m_len = O.Lf + bk;
+    O.an = pm;
+    // walked = every position from the walk start that no match of this chunk covers
+    // (with acceleration: the probed ones, every stride-th from the last match end)
+    bool w = p >= umax(O.q0, pm);
+    if (ACC) w = w && (p - pm < 3u || (p - pm - 2u) % B.stride == 0u);
+    O.walked = wave_ballot(w);
+    W.anchor = umax(anchor0, lane_val(imax, 63));
 }
 
-// Second half: walked positions and match_end - 2 (:680) into the table (never
-// overlapping the producer's lookups, which happen in first halves).
 __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int lane,
                                              const WalkOut &O) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-    if (O.walked && (O.x & X_HASHABLE) && p < B.un) S.tab[O.y >> 16] = (uint16_t)p;
+    const uint2 iv = O.iv;
+    if (((O.walked >> lane) & 1ull) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
+    const bool mem = (O.members >> lane) & 1ull;
+    const uint32_t fwd = O.m_len - O.m_back;      // match length from p
+    // match_end - 2 (:680): hashed by the producer unless the walker extended the match
+    uint32_t e2h = (iv.x >> 16) & (kHSize - 1);
+    bool e2ok = mem && (iv.x & I_E2) && !(iv.x & I_TRUNC);
+    if (mem && (iv.x & I_TRUNC)) {
+        const uint32_t e2 = p + fwd - 2u;
+        if (e2 + 5u <= B.un) {
+            uint32_t lo32 = 0, b4 = 0;
+            for (uint32_t t = 0; t < 5u; t++) {
+                const uint32_t by = B.in[e2 + t];
+                if (t < 4) lo32 |= by << (8 * t); else b4 = by;
+            }
+            e2h = hash5(lo32, b4);
+            e2ok = true;
+        }
+    }
     // one wave's LDS operations complete in order: the walked-position inserts above
     // land before these (compiler barrier only)
     __builtin_amdgcn_sched_barrier(0);
-    const bool mem = O.member;
-    const uint32_t e2 = p + (O.x & 0xFFFFu) - 2u;
-    bool ok = mem && e2 + 5u <= B.un;
-    // the hash ring holds chunks k .. k+3 (positions [64k, 64k + 256)); a match reaching
-    // past it (rare) hashes its bytes itself
-    const bool inring = e2 < 64u * (uint32_t)k + (uint32_t)(kNI * 64);
-    if (wave_any(ok && !inring)) {
-        if (ok && !inring) {
-            const uint32_t at = umin(e2, B.un - 8u);
-            const uint2 v = gload8(B.in + at);
-            const uint32_t sh = e2 - at;
-            S.tab[hash5(__builtin_amdgcn_alignbyte(v.y, v.x, sh), v.y >> (8u * sh))] = (uint16_t)e2;
-        }
-        ok = ok && inring;
+    if (e2ok) S.tab[e2h] = (uint16_t)(p + fwd - 2u);
+    S.wres[k & 1][lane] = make_uint2(O.m_len | (O.m_back << 20), O.an);
+    if (lane == 0) {
+        S.wmem[k & 1][0] = (uint32_t)O.members;
+        S.wmem[k & 1][1] = (uint32_t)(O.members >> 32);
     }
-    if (ok) S.tab[S.hr[e2 & (kNI * 64 - 1)]] = (uint16_t)e2;
 }
 
 // ---------------- emitter ----------------
-// A batch of up to 64 sequences (member i in lane i, in block order) per pass: literal
-// starts from the previous member's end (one lane shift), sizes and output offsets
-// from one wave scan, then every lane writes its own sequence (token, literal length
-// bytes, literals, offset, match length bytes) at its offset.  Sequences that would end
-// past the capacity are not written (the block then fails: result 0).  Two phases, one
-// per half step, so the literal load's latency is covered by the barrier between them.
-struct Em {
-    uint32_t o, ob, oo, lit, ml, off, a;
-    bool ok;
-    int cnt;
-    uint32_t Lw[4];
+// Chunks are emitted in pairs (one 64-byte output window holds ~40 bytes of two
+// chunks' sequences instead of ~20 of one): sizes of each chunk in the second half
+// of step k + 2, both chunks' bytes in the first half of step kA + 4 (kA = the pair's
+// first chunk).
+struct EmitC {          // one chunk's sequences, per member lane
+    uint64_t members;
+    uint32_t tot, ex, an, lit, mo;
+};
+struct Emit {
+    uint32_t o;          // output cursor
+    bool overflow;
+    bool pend;           // A (and B) prepared, not yet written
+    int kA;              // first chunk of the pending pair
+    EmitC A, Bc;
 };
 
-// phase 1; ca / co: the running anchor and output offset (wave-uniform, updated)
-template <bool SMALL>
-__device__ __forceinline__ void emit_load(EncLds &S, const Blk &B, int lane, Em &E, uint32_t &ca,
-                                          uint32_t &co) {
-    E.cnt = (int)__builtin_amdgcn_readfirstlane(S.qcnt);
-    if (E.cnt == 0) return;
-    const bool valid = lane < E.cnt;
-    const uint32_t q0 = S.q[0][lane], q1 = S.q[1][lane];
-    const uint32_t p = q0 & 0xFFFFu, back = q0 >> 16, len = q1 & 0xFFFFu;
-    E.off = q1 >> 16;
-    const uint32_t end = p + len;
-    E.a = wave_shr1(end, ca);                     // previous member's end
-    E.lit = p - back - E.a;
-    E.ml = len + back - kMinMatch;
-    const uint32_t el = ext_bytes(E.lit), em = ext_bytes(E.ml);
-    const uint32_t size = valid ? 3u + E.lit + el + em : 0u;
-    const uint32_t incl = wave_incl_sum(size);
-    E.o = co + incl - size;
-    E.ob = E.o + 1u + el;                         // first literal byte
-    E.oo = E.ob + E.lit;                          // offset
-    E.ok = valid && E.o + size <= B.cap;
-    if (lane == 0) S.qcnt = 0;
-    // up to 16 literals come from one 16-byte load of in[a, a+16) (a + 16 <= n: a
-    // literal run ends at a match start <= n - 12 ... the generic path near the end)
-    ca = lane_val(end, E.cnt - 1);
-    co += lane_val(incl, 63);
-    const bool sl = E.ok && E.lit <= 16u;
-    const uint32_t amax = lane_val(E.a, E.cnt - 1);   // literal starts increase with the lane
-    load16<SMALL>(B.in, B.n, sl ? (int)E.a : 0, E.Lw, !SMALL && amax + 16u <= B.un);
+// Sizes and output offsets of chunk k's sequences into C; `before` = output bytes of
+// the pair's earlier chunk.
+__device__ __forceinline__ void emit_prepare(const EncLds &S, const Blk &B, int k, int lane, Emit &E,
+                                             EmitC &C, uint32_t before) {
+    C.tot = 0;
+    const uint64_t members = ((uint64_t)__builtin_amdgcn_readfirstlane(S.wmem[k & 1][1]) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane(S.wmem[k & 1][0]);
+    C.members = E.overflow ? 0ull : members;
+    if (!C.members) return;
+    const uint2 wr = S.wres[k & 1][lane];
+    const uint32_t off = S.info[k % 3][lane].y & 0xFFFFu;
+    const bool mem = (C.members >> lane) & 1ull;
+    const uint32_t m_len = wr.x & 0xFFFFFu, m_back = wr.x >> 20;
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const uint32_t ms = p - m_back;            // match start after catch-up
+    C.an = wr.y;
+    C.lit = mem ? ms - C.an : 0u;
+    const uint32_t ml = m_len - kMinMatch;
+    const uint32_t size = mem ? 1u + ext_bytes(C.lit) + C.lit + 2u + ext_bytes(ml) : 0u;
+    C.ex = wave_excl_scan(size);
+    C.tot = lane_val(C.ex + size, 63);
+    C.mo = ml | (off << 16);
+    if ((uint64_t)E.o + before + C.tot > B.cap) {
+        E.overflow = true;
+        C.members = 0;
+        C.tot = 0;
+    }
 }
 
-// phase 2: the stores
-__device__ __forceinline__ void emit_store(const Blk &B, int lane, const Em &E) {
-    if (E.cnt == 0) return;
-    // the literal load, once: inside the branchy store sequence below the compiler would
-    // otherwise wait for vmcnt(0) -- every earlier store included -- before each use
-    vm_wait<0>();
-    gu8 *dst = B.dst;
-    const bool ok = E.ok;
-    if (ok) dst[E.o] = (uint8_t)((umin(E.lit, 15u) << 4) | umin(E.ml, 15u));
-    if (wave_any(ok && E.lit >= 15u)) {
-        if (ok) put_len(dst + E.o + 1u, E.lit);
+// Gather the pair (kA, kA + 1).  Lane L of window w produces output byte w + L; its
+// sequence is the last member starting at or before it (owner map + prefix max over
+// owners 1..64 = chunk A's lanes, 65..128 = chunk B's, B's all after A's), whose
+// record comes over by ds_bpermute.  One wave's LDS operations complete in order, so
+// the owner-map writes, the read-back and the clearing need no waits.
+__device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int kA, int lane, Emit &E) {
+    const uint32_t totA = E.A.tot, tot = totA + E.Bc.tot;
+    if (tot == 0) return;
+    const uint32_t P = 64u * (uint32_t)kA;
+    // runs in the first half of step kA + 4, while the producer copies chunk kA + 6
+    // into the ring (or after the last step): input [rlo, P + 384) is intact there
+    const uint32_t rlo = P + 448u > kRingE ? P + 448u - kRingE : 0u;
+    const bool memA = (E.A.members >> lane) & 1ull, memB = (E.Bc.members >> lane) & 1ull;
+    const uint32_t exA = E.A.ex, exB = totA + E.Bc.ex;
+    // member starts, ~0 for other lanes: the window tests below are single compares
+    const uint32_t sA = memA ? exA : 0xFFFFFFFFu, sB = memB ? exB : 0xFFFFFFFFu;
+    gu8 *out = B.dst + E.o;
+    for (uint32_t w = 0; w < tot; w += 64u) {
+        const bool markA = sA - w - 1u < 63u;    // w < start < w + 64
+        const bool markB = sB - w - 1u < 63u;
+        if (markA) ((uint8_t *)S.omap)[exA - w] = (uint8_t)(lane + 1);
+        if (markB) ((uint8_t *)S.omap)[exB - w] = (uint8_t)(lane + 65);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t mk = ((const uint8_t *)S.omap)[lane];
+        __builtin_amdgcn_sched_barrier(0);
+        if (markA) ((uint8_t *)S.omap)[exA - w] = 0;
+        if (markB) ((uint8_t *)S.omap)[exB - w] = 0;
+        const uint64_t covA = wave_ballot(sA <= w);   // member 0 of A starts at 0
+        const uint64_t covB = wave_ballot(sB <= w);
+        const uint32_t carry = covB ? 128u - (uint32_t)__clzll((long long)covB)
+                                    : 64u - (uint32_t)__clzll((long long)covA);
+        const uint32_t own = umax(wave_incl_max(mk), carry) - 1u;
+        const int sl = (int)((own & 63u) << 2);
+        const bool fb = own >= 64u;
+        // all eight permutes by every lane (a permute reads its source lane's register,
+        // so it must not run under a lane-dependent condition), then a select
+        const uint32_t a_ex = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)exA);
+        const uint32_t b_ex = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)exB);
+        const uint32_t a_an = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.an);
+        const uint32_t b_an = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.an);
+        const uint32_t a_li = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.lit);
+        const uint32_t b_li = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.lit);
+        const uint32_t a_mo = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.mo);
+        const uint32_t b_mo = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.mo);
+        const uint32_t r_ex = fb ? b_ex : a_ex, r_an = fb ? b_an : a_an;
+        const uint32_t rl = fb ? b_li : a_li, r_mo = fb ? b_mo : a_mo;
+        const uint32_t b = w + (uint32_t)lane;
+        // every candidate value computed, then selected (no divergent branches)
+        const uint32_t rr = b - r_ex;                    // offset inside the sequence
+        const uint32_t rml = r_mo & 0xFFFFu, roff = r_mo >> 16;
+        const uint32_t lit_at = 1u + ext_bytes(rl), off_at = lit_at + rl;
+        const uint32_t a = r_an + (rr - lit_at);         // literal source position
+        uint32_t v = ((const uint8_t *)S.ring)[a & (kRingE - 1)];
+        if (rr >= lit_at && rr < off_at && a < rlo) v = B.in[a];   // older than the ring (rare)
+        // length extension bytes: 255 while more than 254 remain, then the rest
+        // (the i-th byte after the nibble is min(255, v - 15 - 255 i))
+        const uint32_t vl = umin(rl - 15u - (uint32_t)__umul24(rr - 1u, 255u), 255u);
+        const uint32_t vm = umin(rml - 15u - (uint32_t)__umul24(rr - off_at - 2u, 255u), 255u);
+        const uint32_t vo = rr == off_at ? (roff & 0xFFu) : (roff >> 8);
+        v = rr < off_at ? v : (rr < off_at + 2u ? vo : vm);
+        v = rr < lit_at ? vl : v;
+        v = rr == 0u ? ((umin(rl, 15u) << 4) | umin(rml, 15u)) : v;
+        if (b < tot) out[b] = (uint8_t)v;
     }
-    for (uint64_t lm = wave_ballot(ok && E.lit > 16u); lm; lm &= lm - 1) {   // long runs:
-        const int j = __builtin_ctzll(lm);                                     // the whole wave
-        wave_copy(B.in, dst, lane_val(E.a, j), lane_val(E.ob, j), lane_val(E.lit, j), lane);
-    }
-    const uint32_t nl = (ok && E.lit <= 16u) ? E.lit : 0u;
-#pragma unroll
-    for (uint32_t t = 0; t < 16u; t++) {
-        if (!wave_any(t < nl)) break;
-        if (t < nl) dst[E.ob + t] = (uint8_t)(E.Lw[t >> 2] >> (8u * (t & 3u)));
-    }
-    if (ok) {
-        dst[E.oo] = (uint8_t)E.off;
-        dst[E.oo + 1u] = (uint8_t)(E.off >> 8);
-    }
-    if (wave_any(ok && E.ml >= 15u)) {
-        if (ok) put_len(dst + E.oo + 2u, E.ml);
-    }
+    E.o += tot;
 }
 
 // ---------------- history prefix (withPrefix encode) ----------------
@@ -671,7 +749,8 @@ __device__ __forceinline__ void emit_store(const Blk &B, int lane, const Em &E) 
 // stream, as compress_fast_continue sees it, ref src/ape_lz4.c:1160-1220).  The
 // producer wave hashes every third of them into the table, as loadDict does
 // (:1127-1130; catch-up recovers the bytes a skipped start loses), oldest first (one
-// wave: its LDS writes land in order, so the newest position wins deterministically).
+// wave: its LDS writes land in order, so the newest position wins deterministically),
+// and copies the last 64 into the ring for the first chunk's backward context.
 __device__ __forceinline__ void prefix_history(EncLds &S, const Blk &B, int lane) {
     const uint32_t D = 64u * (uint32_t)B.k0;
     constexpr int kU = 8;   // loads in flight per trip (the loop is latency bound)
@@ -690,177 +769,193 @@ __device__ __forceinline__ void prefix_history(EncLds &S, const Blk &B, int lane
             if (ok[u]) S.tab[hash5(x[u].x, x[u].y)] = (uint16_t)v;
         }
     }
+    const uint32_t p = D - 64u + (uint32_t)lane;
+    const uint8_t by = B.in[p];
+    ((uint8_t *)S.ring)[p & (kRingE - 1)] = by;
+    if (((D - 64u) & (kRingE - 1)) == 0u) ((uint8_t *)S.ring)[kRingE + lane] = by;
 }
 
 // ---------------- block ----------------
-//   step s, first half : producer F(s-1) M(s) H(s+1) L(s+2) | walker walks s-2 |
-//                        emitter writes s-3
-//   step s, second half: walker inserts s-2 into the table and publishes it
-// Table inserts (second half) never overlap the producer's lookups (first half); the
-// info ring slots are s (M), s-1 (F), s-2 (walker), s-3 (emitter): all distinct.
-template <bool SMALL>
+// Three waves per block, one role each, in lock step (two barriers per step):
+//   step s, first half : producer A(s+3) B(s+2) C1(s+1) | walker walks s-1 | emitter writes
+//                                                         |   the pair (s-4, s-3) (every 2nd step)
+//   step s, second half: producer C2(s) -> info[s%3]     | walker inserts s-1, publishes
+//                                                         | emitter sizes s-2
+// Table inserts (second half) never overlap the producer's lookups (first half).
+template <bool SMALL, bool ACC>
 __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, int lane,
                                              int *result) {
     STATS_DECL
     const int k0 = B.k0;
     const int nch = B.nr >= (uint32_t)kMinLength ? B.nch : k0;   // :584, shorter -> last literals only
-    const int nsteps = k0 + ((nch - k0 + 5) & ~1);   // >= nch + 4 steps, even count
+    const int nsteps = k0 + ((nch - k0 + 3) & ~1);   // >= nch + 2 steps (emission lags two)
 
-    if (wave == 1) {   // producer
-        PSet C0, C1;
-        uint32_t XS = 0;   // chunk dword of the chunk in flight between L(k) and H(k)
-        // Load waits (vmcnt counts a wave's loads in issue order).  Issue order per step
-        // s: first half Y(s+1) X(s+2), second half Bc(s) -- one load instruction each
-        // outside SMALL (whose byte loads are waited for whole).
-        // H(s+1): X(s+1) is followed by Bc(s-1): 1 younger.
-        // F(s-1), then M(s): Bc(s-1) (and the older Y(s)) are followed by Y(s+1) X(s+2):
-        // 2 younger.  The step is two halves: H and F run beside the walker's chain, M
-        // beside its table inserts.
-        constexpr int kW1 = SMALL ? 0 : 1, kW2 = SMALL ? 0 : 2;
+    // Each role runs its own loop (same barrier count: 1 + 2 per step), so the
+    // compiler's memory-counter waits in each loop see only that role's operations.
+    if (wave == 1) {
+        PSet P0, P1;
+        // one producer step; `cur` = set of parity s, `nxt` = parity s + 1
         auto pstep = [&](auto fast, int s, PSet &cur, PSet &nxt) {
             constexpr bool F = decltype(fast)::value;
-            // First half: H(s+1) -- the table reads (the walker inserts in second halves)
-            vm_wait<kW1>();                    // X(s+1)
-            x_spread(S, s + 1, lane, XS, nxt.X);
-            p_lookup<SMALL, F>(S, B, s + 1, lane, nxt);
-            p_load<SMALL, F>(B, s + 2, lane, XS);
-            // F(s-1) (info of chunk s-1: read by the walker in step s+1)
-            vm_wait<kW2>();                    // A/Bc(s-1), Y/Z(s)
-            p_finish(S, B, s - 1, lane, nxt);
+            // Every stage runs on every step, past the last chunk too (it then loads
+            // from the block start and records nothing), so the number of loads per
+            // step -- and with it the waits -- is the same on every path.
+            // In flight, oldest first: A(s+2), Y(s+1) x2, E(s) x2 -> A(s+2) at 4.
+            vm_wait<kWin ? 0 : 4>();
+            prod_load<SMALL, F>(B, s + 3, lane, nxt.X);
+            prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
+            // Y(s+1) x2, E(s) x2, A(s+3), Y(s+2) x2 -> Y(s+1) at 5
+            vm_wait<kWin ? 1 : 5>();
+            prod_measure<SMALL, F>(S, B, s + 1, lane, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q, nxt.E);
             STAT(5);
-            __builtin_amdgcn_sched_barrier(0);
             __syncthreads();
             STAT(6);
-            __builtin_amdgcn_sched_barrier(0);
-            // Second half: M(s)
-            p_measure<SMALL, F>(S, B, s, lane, cur);
-#ifdef APE_FINE_STATS
-            STAT(8);
-#endif
-            // nothing may be scheduled across the step boundary: the compiler would
-            // hoist the next step's use of this step's loads above the barrier and
-            // wait for them here
-            __builtin_amdgcn_sched_barrier(0);
-            __syncthreads();
+            // E(s) x2, A(s+3), Y(s+2) x2, E(s+1) x2 -> E(s) at 5
+            vm_wait<kWin ? 1 : 5>();
+            prod_finish(S, B, s, lane, cur.q, cur.E);
             STAT(7);
-            __builtin_amdgcn_sched_barrier(0);
+            __syncthreads();
+            STAT(8);
         };
         if (k0 > 0) prefix_history(S, B, lane);
-        // prologue: the loads in flight at the loop entry in the steady-state order --
-        // Y(k0), X(k0+1), Bc(k0-1) (idle stand-in)
-        p_load<SMALL, false>(B, k0, lane, XS);
+        if (nch > k0) {  // prologue: A(k0), A(k0+1), B(k0), A(k0+2), B(k0+1), C1(k0)
+            prod_load<SMALL>(B, k0, lane, P0.X);
+            prod_load<SMALL>(B, k0 + 1, lane, P1.X);
+            prod_lookup<SMALL>(S, B, k0, lane, P0.X, P0.cT, P0.jL, P0.h, P0.Y);
+            prod_load<SMALL>(B, k0 + 2, lane, P0.X);
+            prod_lookup<SMALL>(S, B, k0 + 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
+            prod_measure<SMALL>(S, B, k0, lane, P0.Y, P0.cT, P0.jL, P0.h, P0.q, P0.E);
+        }
+        // nothing in flight at the loop entry, so the loop's counter waits depend only
+        // on its own issue order (once per block)
         __builtin_amdgcn_s_waitcnt(0);
-        x_spread(S, k0, lane, XS, C0.X);
-        p_lookup<SMALL, false>(S, B, k0, lane, C0);
-        p_load<SMALL, false>(B, k0 + 1, lane, XS);
-        C1.q2 = 0xFFFFFFFFu;
-        C1.lg = 0;
-#pragma unroll
-        for (int t = 0; t < 4; t++) C1.A[t] = 0;
-        load16<SMALL>(B.in, B.n, 0, C1.Bc, !SMALL);
-        __syncthreads();   // table cleared, scratch ready
-        // Steps whose loads all lie inside the block run a loop without edge paths:
-        // X(s+2): 64(s+2)+140 <= n (stage 2 of chunk s reads c + 76 < p + 76 <= n).
-        const int nfast = SMALL || B.n < 268 ? 0 : (B.n - 268) / 64 + 1;
+        __syncthreads();
+        // Steps whose three loads all lie inside the block (A(s+3): 64(s+3)+72 <= n,
+        // Y(s+2): 64(s+2)+91, E(s+1): 64(s+1)+123) run a loop without the edge paths;
+        // the last few steps run the general one.
+        const int nfast_abs = SMALL ? 0 : (int)umin((uint32_t)(B.n >= 264 ? (B.n - 264) / 64 + 1 : 0),
+                                                    (uint32_t)nsteps);
+        const int nfast = nfast_abs > k0 ? k0 + ((nfast_abs - k0) & ~1) : k0;
         int s = k0;
-        // the first step always runs the edge path (chunk k0's backward context)
-        pstep(std::false_type{}, s, C0, C1);
-        pstep(std::false_type{}, s + 1, C1, C0);
-        s += 2;
-        for (; s + 1 < nfast; s += 2) {
-            pstep(std::true_type{}, s, C0, C1);
-            pstep(std::true_type{}, s + 1, C1, C0);
+        for (; s < nfast; s += 2) {   // no conditional step: see pstep
+            pstep(std::true_type{}, s, P0, P1);
+            pstep(std::true_type{}, s + 1, P1, P0);
         }
         for (; s < nsteps; s += 2) {
-            pstep(std::false_type{}, s, C0, C1);
-            pstep(std::false_type{}, s + 1, C1, C0);
+            pstep(std::false_type{}, s, P0, P1);
+            pstep(std::false_type{}, s + 1, P1, P0);
         }
-        __builtin_amdgcn_s_waitcnt(0);
         STATS_FLUSH_TID(g_enc_stats, 64);
         return;
     }
-    if (wave == 0) {   // walker: chunk s-2 during step s
-        // the walker's scalar chain is the latency-critical path of a step: it issues
-        // ahead of the other two roles sharing its SIMD
-        __builtin_amdgcn_s_setprio(3);
+    if (wave == 0) {   // walker: chunk s-1 during step s
         Walk W;
         W.q = 64u * (uint32_t)k0;
-        W.a = W.q;
-        W.qn = 0;
-        W.Q0 = W.Q1 = 0;
-        W.nx = 0;
+        W.anchor = W.q;
+        W.dense = 3u;   // the first search probes 0, 1, 2, then every stride-th
         WalkOut O;
-        O.member = O.walked = false;
-        O.x = O.y = 0;
-        uint2 iv = make_uint2(0u, 0u);   // info of the chunk walked next (read a half early)
         __syncthreads();
         for (int s = k0; s < nsteps; s++) {
-            // chunk s-2 is final: M(s-2) ran in the second half of step s-2, F(s-2) in the
-            // first half of step s-1; its info was read in the second half of step s-1
-            const bool work = s >= k0 + 2 && s - 2 < nch;
-            if (work) walk_chain(B, s - 2, lane, W, O, iv);
+            const bool work = s >= k0 + 1 && s <= nch;
+            if (work) walk_chain<ACC>(S, B, s - 1, lane, W, O);
             STAT(0);
             __syncthreads();
             STAT(4);
-            iv = S.info[(s - 1) & (kNI - 1)][lane];   // chunk s-1: final since F(s-1) above
             if (work) {
-                walk_post(S, s - 2, lane, W, O);
-                walk_publish(S, B, s - 2, lane, O);
+                walk_finish<ACC>(B, s - 1, lane, W, O);
+                walk_publish(S, B, s - 1, lane, O);
+                STAT_ADD(11, __popcll(O.members));
             }
-            // one step after the last chunk: hand over what is still queued (a full batch
-            // may have gone out with the last chunk; the emitter reads it in this step's
-            // first half, and this one in the next step, which exists: nsteps >= nch + 4)
-            if (s - 2 == nch && W.qn) walk_flush(S, lane, W);
+            if (s == nsteps - 1 && lane == 0) S.wend = W.anchor;
             STAT(1);
             STAT_ADD(10, 3);
             __syncthreads();
             STAT(3);
         }
-        STAT_ADD(11, W.nx);
         STATS_FLUSH(g_enc_stats);
         return;
     }
-    // emitter: a batch the walker queued in step s-1, records + literal loads in the
-    // first half of step s, stores in the second
-    __builtin_amdgcn_s_setprio(2);
+    // emitter: sizes of chunk s-2 in the second half of step s (the walker published it
+    // in step s-1); the bytes of a pair (kA, kA+1) in the first half of step kA+4 --
+    // next to the producer's and the walker's long first halves
+    Emit E;
+    E.o = 0;
+    E.overflow = false;
+    E.pend = false;
+    E.kA = k0;
+    E.A.members = E.Bc.members = 0;
+    E.A.tot = E.A.ex = E.A.an = E.A.lit = E.A.mo = 0;
+    E.Bc.tot = E.Bc.ex = E.Bc.an = E.Bc.lit = E.Bc.mo = 0;
     __syncthreads();
-    Em E;
-    uint32_t ca = 64u * (uint32_t)k0, co = 0;   // running anchor / output offset
     for (int s = k0; s < nsteps; s++) {
-        emit_load<SMALL>(S, B, lane, E, ca, co);
+#ifdef APE_EXP_NOEMIT
+        const bool work = false;   // diagnostic: instruction count without the emitter
+#else
+        const bool work = true;
+#endif
+        const int r = s - k0;
+#ifdef APE_EMIT_SINGLE
+        if (work && E.pend && E.kA == s - 3) {   // diagnostic: one chunk per write
+            emit_write(S, B, s - 3, lane, E);
+            E.pend = false;
+        }
+#else
+        if (work && E.pend && E.kA == s - 4) {   // the pair prepared in steps s-2, s-1
+            emit_write(S, B, s - 4, lane, E);
+            E.pend = false;
+        }
+#endif
         STAT(2);
         __syncthreads();
         STAT(14);
-        emit_store(B, lane, E);
-        STAT(12);
-#ifndef APE_FINE_STATS
-        STAT_ADD(8, E.cnt);      // sequences emitted
-        STAT_ADD(9, E.cnt != 0); // batches
+        if (work && r >= 2 && s - 2 < nch) {
+#ifdef APE_EMIT_SINGLE
+            if (true) {
+#else
+            if (((r - 2) & 1) == 0) {            // first chunk of a pair
 #endif
+                E.Bc.members = 0;
+                E.Bc.tot = 0;
+                emit_prepare(S, B, s - 2, lane, E, E.A, 0u);
+                E.kA = s - 2;
+                E.pend = true;
+            } else {
+                emit_prepare(S, B, s - 2, lane, E, E.Bc, E.A.tot);
+            }
+        }
+        STAT(12);
         __syncthreads();
         STAT(15);
     }
-    // ---- last literals (:732-751), from the final anchor ----
-    const uint32_t anchor = ca;
-    const uint32_t o = co;
-    const uint32_t lit = B.un - anchor;
-    const uint32_t hdr = 1u + ext_bytes(lit);
-    const uint32_t total = o + hdr + lit;
-    const bool overflow = total > B.cap;
-    if (!overflow) {
-        if (lane == 0) {
-            B.dst[o] = (uint8_t)((lit < 15u ? lit : 15u) << 4);
-            put_len(B.dst + o + 1, lit);
+    // the last pair may still be pending (its write step lies past the loop)
+    if (E.pend) emit_write(S, B, E.kA, lane, E);
+    // ---- last literals (:732-751), from the walker's final anchor ----
+    if (!E.overflow) {
+        const uint32_t anchor = S.wend;
+        const uint32_t lit = B.un - anchor;
+        const uint32_t hdr = 1u + ext_bytes(lit);
+        const uint32_t total = E.o + hdr + lit;
+        if (total > B.cap) {
+            E.overflow = true;
+        } else {
+            if (lane == 0) {
+                B.dst[E.o] = (uint8_t)((lit < 15u ? lit : 15u) << 4);
+                put_len(B.dst + E.o + 1, lit);
+            }
+            wave_copy(B.in, B.dst, anchor, E.o + hdr, lit, lane);
+            E.o = total;
         }
-        wave_copy(B.in, B.dst, anchor, o + hdr, lit, lane);
     }
-    if (lane == 0) *result = overflow ? 0 : (int)total;
+    if (lane == 0) *result = E.overflow ? 0 : (int)E.o;
     STAT_ADD(13, 1);
     STATS_FLUSH_TID(g_enc_stats, 128);
 }
 
 }  // namespace
 
+// ACC: compress_fast with acceleration > 1 (its own instantiation, so the default
+// kernel carries none of the probe-pattern code)
+template <bool ACC>
 __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(6)))
 lz4_encode_kernel(BlockArgs a) {
     __shared__ EncLds S;
@@ -892,8 +987,12 @@ lz4_encode_kernel(BlockArgs a) {
     B.nr = (uint32_t)nr;
     B.k0 = D / 64;
     // compress_fast's acceleration (:789-808) trades ratio for speed; here that is the
-    // in-chunk candidate
-    B.noL = a.accel > 1;
+    // in-chunk candidate (-11 % encode time, ratio -1.7 % on App. C data)
+    B.noL = ACC;
+    B.stride = ACC ? (a.accel < (1 << 20) ? (uint32_t)a.accel : 1u << 20) : 1u;
+    B.pat = 0;
+    if (ACC)
+        for (uint32_t i = 0; i < 64u; i += B.stride) B.pat |= 1ull << i;
     B.cap = (uint32_t)icap;
     B.un = (uint32_t)B.n;
     B.mstart = B.un >= 12 ? B.un - 12 : 0;   // matches start at <= n-12 (:585)
@@ -902,24 +1001,26 @@ lz4_encode_kernel(BlockArgs a) {
 
     // table = 0 (the reference's memset state: position 0 for every hash)
     for (int i = tid; i < kHSize / 8; i += 192) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
-    if (tid < 64) S.scr[tid] = 0xFFFFFFFFu;
-    if (tid == 0) S.qcnt = 0;
+    for (int i = tid; i < (int)kScr; i += 192) S.scr[i] = 0xFFFFFFFFu;
+    for (int i = tid; i < (int)(kRingE / 16 + 4); i += 192) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
+    if (tid < 16) S.omap[tid] = 0u;
     __syncthreads();
-    if (B.n < kSmall) encode_block<true>(S, B, wave, lane, &a.result[b]);
-    else encode_block<false>(S, B, wave, lane, &a.result[b]);
+    if (B.n < kSmall) encode_block<true, ACC>(S, B, wave, lane, &a.result[b]);
+    else encode_block<false, ACC>(S, B, wave, lane, &a.result[b]);
 }
 
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
-    // The round-1 encoder (lz4_encode_v1.hip) stays the product path until this
-    // three-role pipeline beats it (A/B: tools/gpu_enc_ab.sh); APE_LZ4_ENCODER=v2
-    // selects this one.
+    // APE_LZ4_ENCODER=v2: the three-role v2 pipeline (lz4_encode_v2.hip), A/B only
     static const int v2 = [] {
         const char *e = getenv("APE_LZ4_ENCODER");
         return e && e[0] == 'v' && e[1] == '2' ? 1 : 0;
     }();
-    if (!v2) return launch_encode_v1(a, s);
-    hipLaunchKernelGGL(lz4_encode_kernel, dim3(a.nblocks), dim3(192), 0, s, a);
+    if (v2 && a.accel <= 1) return launch_encode_v2(a, s);
+    if (a.accel > 1)
+        hipLaunchKernelGGL(lz4_encode_kernel<true>, dim3(a.nblocks), dim3(192), 0, s, a);
+    else
+        hipLaunchKernelGGL(lz4_encode_kernel<false>, dim3(a.nblocks), dim3(192), 0, s, a);
     return hipGetLastError();
 }
 
