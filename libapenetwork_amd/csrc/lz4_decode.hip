@@ -20,13 +20,17 @@
 //         are parsed by the scalar restatement of the reference loop instead.
 //         Accepted sequences become descriptors {literal source, output
 //         position, literal length, offset} in LDS.
-//  COPY   The batch's output is produced in 256-byte steps, 4 bytes per lane.
-//         A byte is a literal (staged compressed bytes, or the block in HBM for
-//         long literal runs), or a match byte whose source -- reduced modulo the
-//         offset to lie before the match -- is older than `gdone` (stored to dst
-//         and drained by vmcnt(0): read back bypassing this CU's L1), newer (the
-//         LDS history ring), or inside this step (resolved through the step's
-//         owner map).  Output goes to the ring and straight to dst.
+//  COPY   One lane per sequence: the batch's output is assembled in an LDS window
+//         of recent output.  Round 1: every lane writes its literal run (16-byte
+//         LDS read from the staged input, exact-length write) and its match when the
+//         match's sources precede the batch -- up to four 16-byte units read from the
+//         window, or from dst history (flushed, drained, read bypassing this CU's L1),
+//         or the external dictionary.  Matches whose sources lie inside the batch wait
+//         for the rounds that follow: everything before the first pending sequence is
+//         final, so each round copies every pending match whose sources end there.
+//         Long runs, offsets < 16 inside their own output and sources straddling the
+//         window start are copied by the whole wave.  The window is then flushed to
+//         dst with coalesced 16-byte stores.
 // Decoded blocks are not limited to 64 KiB: only the 64 KiB offset window is.
 #include "lz4_gpu_internal.h"
 #include <type_traits>
@@ -35,25 +39,73 @@ namespace apelz4 {
 
 namespace {
 
-#ifndef APE_LZ4_DRING
-#define APE_LZ4_DRING 1024
+// Output window (LDS): the batch's output is assembled in a linear window of recent
+// output and flushed to dst with coalesced 16-byte stores.  When a batch would run past
+// its end, the window slides: the last kKeep bytes move to its start, and everything
+// older is read back from dst (flushed and drained by then).
+#ifndef APE_LZ4_DWIN
+#define APE_LZ4_DWIN 4096
 #endif
-constexpr int kRing = APE_LZ4_DRING;  // per-wave history ring (bytes, power of two)
+#ifndef APE_LZ4_DKEEP
+#define APE_LZ4_DKEEP 1024
+#endif
+constexpr uint32_t kWinB = APE_LZ4_DWIN;   // output window bytes
+constexpr uint32_t kKeep = APE_LZ4_DKEEP;  // history kept when the window slides
+static_assert(kKeep >= 64 && kKeep % 16 == 0 && kWinB >= kKeep + 1024 && kWinB % 16 == 0,
+              "output window");
 constexpr int kStage = 2304;     // staged compressed bytes per batch (9 dwords/lane)
 constexpr int kWinNeed = 84;     // a parse window reads up to P + 63 + 21
-constexpr int kStep = 256;       // output bytes per copy step (4 per lane)
 constexpr int kMaxDesc = 64;     // descriptors per batch
 constexpr int kFlushAt = 40;     // copy once a batch holds more than this (window adds <= 22)
-constexpr int kMaxCarry = 24;    // descriptors carried into the next batch (< kFlushAt)
+constexpr uint32_t kLaneMax = 64;  // longest match one lane copies (4 x 16 bytes)
 
 struct __attribute__((aligned(16))) WaveLds {
-    uint8_t ring[kRing];
+    uint8_t win[kWinB + 64];     // output [base, base + kWinB) (+ slack for 16-byte reads)
     uint8_t stage[kStage + 16];  // src[s0 .. s0 + kStage), zero beyond the input
     uint4 desc[kMaxDesc];        // {lit_src, out, lit_len, offset}
-    uint32_t own[kStep / 4];     // owner map of the current step (u8 per byte)
 };
 
+// unaligned LDS accesses (gfx950 DS instructions take any byte address)
+typedef uint32_t l32x4 __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t l32x2 __attribute__((ext_vector_type(2), aligned(1)));
+typedef uint32_t l32 __attribute__((aligned(1)));
+typedef uint16_t l16 __attribute__((aligned(1)));
 
+__device__ __forceinline__ uint4 lds16(const uint8_t *p) {
+    const l32x4 v = *(const l32x4 *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void lds_st16(uint8_t *p, uint4 v) {
+    l32x4 w;
+    w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+    *(l32x4 *)p = w;
+}
+// dword k (0..3) of v
+__device__ __forceinline__ uint32_t dw4(uint4 v, uint32_t k) {
+    return (k & 2u) ? ((k & 1u) ? v.w : v.z) : ((k & 1u) ? v.y : v.x);
+}
+// Exactly n (1..15) bytes of v at p, as the pieces 8/4/2/1 of n.  A piece n lacks is
+// written anyway at offset 0 (the same bytes are there) whenever n >= its size, so only
+// pieces larger than n need a branch (none when MIN4 says n >= 4 and n >= 8).
+template <bool MIN4>
+__device__ __forceinline__ void lds_put_small(uint8_t *p, uint4 v, uint32_t n) {
+    const uint32_t a4 = (n & 4u) ? (n & 8u) : 0u;
+    const uint32_t a2 = (n & 2u) ? (n & 12u) : 0u;
+    const uint32_t a1 = (n & 1u) ? (n & 14u) : 0u;
+    if (n >= 8u) {
+        l32x2 t;
+        t.x = v.x; t.y = v.y;
+        *(l32x2 *)p = t;
+    }
+    if (MIN4 || n >= 4u) *(l32 *)(p + a4) = dw4(v, a4 >> 2);
+    if (MIN4 || n >= 2u) *(l16 *)(p + a2) = (uint16_t)(dw4(v, a2 >> 2) >> (8u * (a2 & 2u)));
+    p[a1] = (uint8_t)(dw4(v, a1 >> 2) >> (8u * (a1 & 3u)));
+}
+// 16 bytes of dst history, bypassing this CU's L1 (stores of this wave reach L2 only)
+__device__ __forceinline__ uint4 gload16_nt(gcu8 *p) {
+    const u32x4_u v = __builtin_nontemporal_load((__attribute__((address_space(1))) const u32x4_u *)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
@@ -192,48 +244,102 @@ __device__ int parse_scalar(WaveLds &L, const Dec &D, int &ip, uint32_t &op, int
     return ST_MORE;
 }
 
-// One speculative window at P (P - s0 + kWinNeed <= kStage): appends the
-// chain's descriptors.  Returns ST_MORE with P advanced (to the next token, or
-// to a complex token when `cplx`), or ST_DONE / ST_ERR with `res`.
-template <bool PARTIAL, bool DICT, bool FASTD = false>
-__device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int &nd, int &res,
-                            bool &cplx) {
-    const int lane = D.lane;
-    const uint32_t r = (uint32_t)(P - D.s0 + lane);
+// lane l receives v of lane idx (0..63)
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t idx) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(idx << 2), (int)v);
+}
+
+// The sequence that would start at window position rel (token at P + rel), parsed
+// speculatively from the staged bytes: token, literal length, offset, one match-length
+// extension byte, and where the next token would be.
+struct Spec {
+    uint32_t lit, off, ml;
+    int ipl, ipo, q;                 // first literal byte, after the offset, next token
+    bool fin_in, mlerr, cx;          // input ends in the literals / ml bytes run out / complex
+};
+
+template <bool FASTD>
+__device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, uint32_t rel) {
+    Spec z;
+    const uint32_t r = (uint32_t)(P - D.s0) + rel;
     const uint32_t tok = L.stage[r];
     const uint32_t lit = tok >> 4, mn = tok & 15u;
     const uint32_t r1 = r + 1u + lit;           // offset bytes (then the ml byte)
     const uint32_t a1 = r1 & ~3u;
     const uint32_t x = funnel(*(const uint32_t *)&L.stage[a1 + 4], *(const uint32_t *)&L.stage[a1],
                               r1 & 3u);
-    const uint32_t off = x & 0xFFFFu, e = (x >> 16) & 0xFFu;
-    const int p = P + lane;
-    const int ipl = p + 1;                       // first literal byte
-    const int ipo = ipl + (int)lit + 2;          // after the offset
-    const bool fin_in = !FASTD && (uint32_t)ipl + lit + 8u > (uint32_t)D.csize;   // ipl >= 1
+    const uint32_t e = (x >> 16) & 0xFFu;
+    z.lit = lit;
+    z.off = x & 0xFFFFu;
+    z.ipl = P + (int)rel + 1;
+    z.ipo = z.ipl + (int)lit + 2;
+    z.fin_in = !FASTD && (uint32_t)z.ipl + lit + 8u > (uint32_t)D.csize;   // ipl >= 1
     const bool mlx = mn == 15u;
-    const bool mlerr = !FASTD && mlx && ipo + kLastLiterals > D.csize;
-    const bool cx = lit == 15u || (mlx && e == 255u && !mlerr);
-    const uint32_t ml = mlx ? 15u + e : mn;
-    const int q = ipo + (mlx ? 1 : 0);           // next token
-    // hop to the next token (relative to P); a final / failing sequence ends the
-    // chain (kHopTerm), a complex token ends it before itself (kHopCplx)
-    constexpr uint32_t kHopTerm = 0x80u, kHopCplx = 0xC0u;
-    const uint32_t hop = cx ? kHopCplx : ((fin_in || mlerr) ? kHopTerm : (uint32_t)(q - P));
+    z.mlerr = !FASTD && mlx && z.ipo + kLastLiterals > D.csize;
+    z.cx = lit == 15u || (mlx && e == 255u && !z.mlerr);
+    z.ml = mlx ? 15u + e : mn;
+    z.q = z.ipo + (mlx ? 1 : 0);
+    return z;
+}
 
-    // follow the chain from P (scalar: one v_readlane per sequence, 4 instructions)
-    uint32_t c = 0, last = 0;
-    uint64_t M = 0;
-    do {
-        last = c;
-        M |= 1ull << c;
-        c = (uint32_t)__builtin_amdgcn_readlane((int)hop, (int)c);
-    } while (c < 64u);
-    cplx = c == kHopCplx;
-    if (cplx) M &= ~(1ull << last);           // the complex token is not a member
-    if (c >= kHopTerm) c = last;              // (P is not advanced past a final token)
+// One speculative window at P (P - s0 + kWinNeed <= kStage): appends the chain's
+// descriptors.  Returns ST_MORE with P advanced (to the next token, or to a complex
+// token when `cplx`), or ST_DONE / ST_ERR with `res`.
+//
+// Every lane parses "the sequence at P + lane" and its successor (hop).  The true
+// chain from P is found by binary lifting instead of a serial walk: J_k = hop^(2^k)
+// (four ds_bpermute rounds), and lane t composes them by the bits of t into the
+// position of the chain's t-th sequence (a window holds <= 22: each sequence takes
+// >= 3 input bytes).  Lane t then re-reads its member from the staged bytes, so the
+// members arrive compacted and in order.
+template <bool PARTIAL, bool DICT, bool FASTD = false>
+__device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int &nd, int &res,
+                            bool &cplx) {
+    const int lane = D.lane;
+    // a final / failing sequence ends the chain (kHopTerm), a complex token ends it
+    // before itself (kHopCplx); every exit value is >= 64 and absorbs
+    constexpr uint32_t kHopTerm = 0x80u, kHopCplx = 0xC0u;
+    uint32_t hop;
+    {
+        const Spec z = spec_at<FASTD>(L, D, P, (uint32_t)lane);
+        hop = z.cx ? kHopCplx : ((z.fin_in || z.mlerr) ? kHopTerm : (uint32_t)(z.q - P));
+    }
+    auto jump = [](uint32_t J, uint32_t idx) {
+        const uint32_t g = bperm(J, idx & 63u);
+        return idx < 64u ? g : idx;
+    };
+    const uint32_t J1 = jump(hop, hop);
+    const uint32_t J2 = jump(J1, J1);
+    const uint32_t J3 = jump(J2, J2);
+    const uint32_t J4 = jump(J3, J3);
+    const uint32_t t = (uint32_t)lane;
+    uint32_t pos = (t & 1u) ? lane_val(hop, 0) : 0u;
+    {
+        const uint32_t p2 = jump(J1, pos);
+        pos = (t & 2u) ? p2 : pos;
+        const uint32_t p4 = jump(J2, pos);
+        pos = (t & 4u) ? p4 : pos;
+        const uint32_t p8 = jump(J3, pos);
+        pos = (t & 8u) ? p8 : pos;
+        const uint32_t p16 = jump(J4, pos);
+        pos = (t & 16u) ? p16 : pos;
+    }
+    pos = t < 32u ? pos : kHopTerm;
+    const int cnt = __popcll(wave_ballot(pos < 64u));   // chain members: lanes [0, cnt)
+    const uint32_t X = lane_val(pos, cnt);               // the chain's exit
+    const uint32_t lastp = lane_val(pos, cnt - 1);
+    cplx = X == kHopCplx;
+    const int nm = cplx ? cnt - 1 : cnt;                 // the complex token is not a member
+    const uint32_t c = X >= kHopTerm ? lastp : X;        // (P is not advanced past a final token)
+    const uint64_t M = (1ull << nm) - 1ull;              // nm <= 22
+
+    // member t = the sequence at P + pos, re-read from the staged bytes
+    const bool mem = (int)t < nm;
+    const Spec z = spec_at<FASTD>(L, D, P, mem ? pos : 0u);
+    const uint32_t lit = z.lit, ml = z.ml, off = z.off;
+    const int ipl = z.ipl, ipo = z.ipo, q = z.q;
+    const bool fin_in = z.fin_in, mlerr = z.mlerr;
     // output positions, checks in the reference's order
-    const bool mem = (M >> lane) & 1ull;
     const uint32_t ob = mem ? (fin_in ? lit : lit + ml + kMinMatch) : 0u;
     const uint32_t ex = wave_excl_scan(ob);
     const uint32_t opl = op + ex;
@@ -260,7 +366,7 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const bool bad = fin ? (badfin || e_in) : stop;
     const int rv = fin ? ((badfin || e_in) ? -ipl - 1 : (int)(FASTD ? iend : cpy))
                        : ((e_off || mlerr) ? -ipo - 1 : -q - 1);
-    const uint64_t sm = wave_ballot(mem && stop) & M;
+    const uint64_t sm = wave_ballot(mem && stop);
     uint64_t emit = M;
     int st = ST_MORE;
     if (sm) {
@@ -268,228 +374,296 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
         res = (int)lane_val((uint32_t)rv, T);
         const bool tbad = lane_val(bad ? 1u : 0u, T) != 0u;
         // members before T (error) or up to T (final literals)
-        if (tbad) emit = M & ((1ull << T) - 1ull);
-        else emit = M & (T == 63 ? ~0ull : ((2ull << T) - 1ull));
+        emit = tbad ? ((1ull << T) - 1ull) : ((2ull << T) - 1ull);   // T <= 21
         st = tbad ? ST_ERR : ST_DONE;
         cplx = false;
     }
     if (st != ST_ERR) {
-        if ((emit >> lane) & 1ull) {
-            const uint32_t idx = (uint32_t)nd + __builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(emit >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)emit, 0u));
-            L.desc[idx] = make_uint4((uint32_t)ipl, opl, lit, fin ? 0u : off);
-        }
-        nd += __popcll(emit);
-        if (emit) {
-            const int last = 63 - __clzll((long long)emit);
+        const int ne = __popcll(emit);
+        if ((int)t < ne) L.desc[nd + lane] = make_uint4((uint32_t)ipl, opl, lit, fin ? 0u : off);
+        nd += ne;
+        if (ne) {
             // a final sequence's size is its literals (ob assumed a match unless the
             // input ended: a PARTIAL or FASTD stop by output size ends the block too)
-            op = lane_val(opl + (fin ? lit : ob), last);
+            op = lane_val(opl + (fin ? lit : ob), ne - 1);
         }
     }
     if (st == ST_MORE) P += (int)c;
     return st;
 }
 
-// x mod off for x < off + 3 (three conditional subtractions cover off = 1)
-__device__ __forceinline__ uint32_t reduce3(uint32_t x, uint32_t off) {
-    x = x >= off ? x - off : x;
-    x = x >= off ? x - off : x;
-    return x >= off ? x - off : x;
+// ---------------- copy: descriptors -> output window -> dst ----------------
+// The window holds output positions [base, base + kWinB); dst[0, fl) is flushed and
+// dst[0, gdone) flushed and drained (readable as history; gdone >= base + kKeep - 15
+// once the window has slid, so every position below base is readable from dst).
+struct Win {
+    uint32_t base, fl, gdone;
+};
+
+// Literal run of one sequence, copied by the whole wave: n bytes from input position
+// src to output position at (16-byte units; the last unit ends exactly at n and
+// overlaps its neighbour with the same bytes, so nothing outside [at, at + n) is written).
+__device__ __forceinline__ void coop_literal(WaveLds &L, const Dec &D, uint32_t base, uint32_t at,
+                                             uint32_t n, uint32_t src) {
+    const int lane = D.lane;
+    uint8_t *w = L.win + (at - base);
+    const uint32_t rs = src - (uint32_t)D.s0;
+    const bool staged = rs < (uint32_t)kStage && rs + n <= (uint32_t)kStage;   // wave-uniform
+    if (n >= 16u) {
+        for (uint32_t t = 16u * (uint32_t)lane; t < n; t += 1024u) {
+            const uint32_t tt = umin(t, n - 16u);
+            const uint4 v = staged ? lds16(L.stage + rs + tt) : gload16(D.src + (src + tt));
+            lds_st16(w + tt, v);
+        }
+    } else if ((uint32_t)lane < n) {
+        w[lane] = staged ? L.stage[rs + lane] : D.src[src + (uint32_t)lane];
+    }
 }
 
-// Produce output [lo, hi) of the step at `base` from the batch's descriptors.
-// Branch-light: every byte gets an LDS address and (rarely) an HBM pointer; loads
-// are guarded by wave-uniform tests only, so the wave does not juggle exec masks.
+// Match of one sequence copied by the whole wave, 64 bytes per pass in order (every
+// source precedes its byte: offset >= 64 reads earlier passes, a shorter offset reads
+// the match's first period).  Sources: the window (>= base), dst history (< base) or
+// the external dictionary (< 0).  Used for what the lane path does not take: long
+// matches, offsets < 16 inside their own output, sources straddling the window start.
 template <bool DICT>
-__device__ __forceinline__ void copy_step(WaveLds &L, const Dec &D, uint32_t base, uint32_t lo,
-                                          uint32_t hi, uint32_t gdone, int nd, uint32_t d_out,
-                                          uint32_t &diag) {
+__device__ __forceinline__ void coop_match(WaveLds &L, const Dec &D, uint32_t base, uint32_t ma,
+                                        uint32_t n, uint32_t off) {
     const int lane = D.lane;
-    // owner map: mark descriptor starts inside (lo, hi); the one covering lo carries in
-    const uint32_t cur = (uint32_t)__popcll(wave_ballot(d_out <= lo)) - 1u;   // d_out = ~0 past nd
-    L.own[lane] = 0u;
-    wave_sync();
-    if (d_out - lo - 1u < hi - lo - 1u) ((uint8_t *)L.own)[d_out - base] = (uint8_t)(lane + 1);  // lo < d_out < hi
-    wave_sync();
-    const uint32_t m = L.own[lane];
-    const uint32_t run = umax(umax(m & 0xFFu, (m >> 8) & 0xFFu), umax((m >> 16) & 0xFFu, m >> 24));
-    const uint32_t pre = umax(wave_shr1(wave_incl_max(run), 0u), cur + 1u);
-    const uint32_t A = pre - 1u;
-    const bool hasB = A + 1u < (uint32_t)nd;
-    const uint4 dA = L.desc[A];
-    const uint4 dB = L.desc[hasB ? A + 1u : A];
-    const uint32_t outB = hasB ? dB.y : 0xFFFFFFFFu;
-    const uint32_t leA = dA.y + dA.z, leB = dB.y + dB.z;
-    const uint32_t xlA = dA.x - dA.y, xlB = dB.x - dB.y;   // literal source - output
-    const uint32_t offA = dA.w, offB = dB.w;
-    const uint32_t s0 = (uint32_t)D.s0;
-    const uint32_t q0 = base + 4u * (uint32_t)lane;
-
-    // offset of byte 0 inside A's match period (one division, only if some lane needs it)
-    uint32_t rA = q0 - leA;                       // valid when q0 >= leA
-    const bool needmod = q0 >= leA && offA != 0u && rA >= offA;
-    if (wave_any(needmod)) {
-        diag |= 1u;
-        if (needmod) rA %= offA;
+    uint8_t *w = L.win + (ma - base);
+    if (off == 0u) {   // offset 0 decodes as zero bytes
+        for (uint32_t t = (uint32_t)lane; t < n; t += 64u) w[t] = 0;
+        return;
     }
-
-    // per byte: source position, LDS address (kNone = a zero byte), HBM kind (1 src,
-    // 2 dst, 3 dictionary).  Two wave-uniform specialisations: FULL (the step is
-    // produced whole: no range test) and SO (some lane's offset is 1..3: its period
-    // needs up to three reductions; otherwise one conditional subtraction covers
-    // rA + j < off + 3 and q - le <= 2).
-    constexpr uint32_t kNone = (uint32_t)offsetof(WaveLds, stage) + (uint32_t)kStage;
-    uint32_t pos[4], lad[4], gk[4];
-    uint32_t pendm = 0;
-    bool anyg = false;
-    auto bytes = [&](auto so_t, auto full_t) {
-        constexpr bool SO = decltype(so_t)::value, FU = decltype(full_t)::value;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            // Every arm is computed into a variable first and the ternaries only pick
-            // between plain values: the compiler then emits v_cndmask selects, not the
-            // divergent branches (exec-mask juggling on the scalar unit) that nested
-            // ternaries with arithmetic in their arms become.
-            const uint32_t q = q0 + j;
-            const bool inB = q >= outB;
-            const uint32_t le = inB ? leB : leA, off = inB ? offB : offA, xl = inB ? xlB : xlA;
-            const bool lit = q < le;
-            const uint32_t mbB = q - leB, mbA0 = rA + j, mbA1 = q - leA;
-            const uint32_t mbA = q0 >= leA ? mbA0 : mbA1;
-            const uint32_t mb = inB ? mbB : mbA;
-            const uint32_t red = SO ? reduce3(mb, off) : umin(mb, mb - off);
-            const uint32_t mpos = le - off + red;
-            const uint32_t lpos = q + xl;
-            const uint32_t ps = lit ? lpos : mpos;
-            const bool live = (FU || (q >= lo && q < hi)) && (lit || off != 0u);  // offset 0 -> 0
-            const bool inst = ps - s0 < (uint32_t)kStage;
-            // DICT: a match source before the block start ("negative" ps) is in the dictionary
-            const bool hist = DICT && ps >= 0x80000000u;
-            const bool ring = !lit && !hist && ps >= gdone && ps < lo;
-            const bool pend = live && !lit && !hist && ps >= lo;
-            const uint32_t a_st = ps - s0 + (uint32_t)offsetof(WaveLds, stage), a_rg = ps & (kRing - 1);
-            const uint32_t a_lit = inst ? a_st : kNone, a_mat = ring ? a_rg : kNone;
-            const uint32_t a_live = lit ? a_lit : a_mat;
-            pos[j] = ps;
-            lad[j] = live ? a_live : kNone;
-            const uint32_t g_old = ps < gdone ? 2u : 0u;
-            const uint32_t g_lit = inst ? 0u : 1u, g_mat = hist ? 3u : g_old;
-            const uint32_t g_live = lit ? g_lit : g_mat;
-            gk[j] = (live && !pend) ? g_live : 0u;
-            anyg |= gk[j] != 0u;
-            pendm |= pend ? 1u << j : 0u;
+    const bool per = off < 64u;                     // wave-uniform
+    uint32_t r = per ? (uint32_t)lane % off : 0u;   // (t - ma) mod off for t = lane
+    const uint32_t inc = per ? 64u % off : 0u;
+    for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
+        const uint32_t t = t0 + (uint32_t)lane;
+        if (t < n) {
+            const int sp = per ? (int)ma - (int)off + (int)r : (int)(ma + t) - (int)off;
+            uint32_t v;
+            if (sp >= (int)base) v = L.win[(uint32_t)sp - base];
+            else if (DICT && sp < 0) v = D.dend[sp];
+            else v = __builtin_nontemporal_load(D.dst + sp);
+            w[t] = (uint8_t)v;
         }
-    };
-    const bool so = offA - 1u < 3u || offB - 1u < 3u;
-    const bool full = lo == base && hi == base + kStep;
-    if (wave_any(so)) {
-        if (full) bytes(std::true_type{}, std::true_type{});
-        else bytes(std::true_type{}, std::false_type{});
-    } else {
-        if (full) bytes(std::false_type{}, std::true_type{});
-        else bytes(std::false_type{}, std::false_type{});
-    }
-    // fetch: LDS for every byte, HBM only if a lane needs it (an in-step source
-    // reads 0 here and is filled in below)
-    const uint8_t *lds = (const uint8_t *)&L;
-    uint32_t v[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) v[j] = lds[lad[j]];   // kNone reads 0
-    if (wave_any(anyg)) {
-        diag |= 0x10000u;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            // one nontemporal byte load for both sources (history in dst must bypass
-            // this CU's L1; the literal in src does not care); idle lanes read src[0].
-            // A/B (tools/dec_variants.sh, 65536 blocks): device-scope loads that allocate
-            // in L2 fetch as much (the history misses L2 either way: ~1000 blocks per XCD
-            // stream their output through its 4 MB) and take 12% longer.
-            gcu8 *bp = gk[j] == 2u ? (gcu8 *)D.dst : D.src;
-            const uint32_t o = gk[j] != 0u ? pos[j] : 0u;
-            if (DICT && gk[j] == 3u) bp = D.dend - 0x100000000ll;   // dend + (int32)o
-            const uint32_t g = __builtin_nontemporal_load(bp + o);
-            v[j] = gk[j] != 0u ? g : v[j];
-        }
-    }
-    // In-step sources.  A pending byte's source (already reduced into the match's first
-    // period) is an earlier byte of this step.  The step's resolved bytes go to the
-    // ring, with a done flag per byte in the (no longer needed) owner map; each pass
-    // then copies every pending byte whose source is done.  Sources strictly precede
-    // their bytes, so each pass resolves at least the lowest pending byte of the step,
-    // and one pass usually resolves all.  No byte of this step reads the ring slots it
-    // overwrites (ring sources lie in [gdone, lo), and lo - gdone <= 512).
-#ifdef APE_DEXP_NOPEND
-    if (false) {   // diagnostic: instruction count without in-step sources (wrong bytes)
-#else
-    if (wave_any(pendm != 0)) {
-#endif
-        diag |= 2u;
-        uint8_t *ring = L.ring;
-        uint8_t *done = (uint8_t *)L.own;
+        r += inc;
+        r = r >= off ? r - off : r;
         wave_sync();
-        uint32_t dw = 0;
-        if (lo == base && hi == base + kStep) {   // whole step: one dword (pending bytes 0)
-            *(uint32_t *)&ring[q0 & (kRing - 1)] = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t q = q0 + j;
-                if (q >= lo && q < hi) ring[q & (kRing - 1)] = (uint8_t)v[j];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) dw |= ((pendm >> j) & 1u) ? 0u : 1u << (8 * j);
-        L.own[lane] = dw;
-        wave_sync();
-        while (wave_any(pendm != 0)) {
-            diag += 4u;
-            uint32_t now = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t src = pos[j];
-                const bool pj = (pendm >> j) & 1u;
-                const uint32_t dn = done[pj ? src - base : 0u];
-                const uint32_t val = ring[src & (kRing - 1)];
-                const bool ok = pj && dn != 0u;
-                v[j] = ok ? val : v[j];
-                now |= ok ? 1u << j : 0u;
-            }
-            wave_sync();
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                if ((now >> j) & 1u) {
-                    const uint32_t q = q0 + j;
-                    ring[q & (kRing - 1)] = (uint8_t)v[j];
-                    done[q - base] = 1u;
-                }
-            }
-            pendm &= ~now;
-            wave_sync();
-        }
     }
-    const uint32_t word = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
-    wave_sync();
-    // store: ring and dst (the whole-step case is uniform)
-    gu8 *o8 = D.dst + q0;
-    if (lo == base && hi == base + kStep) {
-        *(uint32_t *)&L.ring[q0 & (kRing - 1)] = word;
-        if ((((uintptr_t)(D.dst + base)) & 3u) == 0) {
-            *(__attribute__((address_space(1))) uint32_t *)o8 = word;
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; j++) o8[j] = (uint8_t)(word >> (8 * j));
-        }
+}
+
+// Match of this lane's sequence (n <= 64 bytes at output ma, offset off), for the
+// lanes with `go`: up to four 16-byte units (the last one ends exactly at n), read
+// first and then written when the sources precede ma, unit after unit when the match
+// overlaps itself (offset 16..n-1), or exactly n bytes when n < 16.  `glb`: the source
+// is dst history / the dictionary instead of the window.
+template <bool DICT>
+__device__ __forceinline__ void lane_match(WaveLds &L, const Dec &D, uint32_t base, bool go,
+                                           uint32_t ma, uint32_t n, uint32_t off, bool glb) {
+    if (!go) return;
+    uint8_t *w = L.win + (ma - base);
+    const int ps = (int)ma - (int)off;
+    const bool big = n >= 16u;
+    // unit offsets: 0, 16, 32, 48 clamped to n - 16 (repeats rewrite the same bytes)
+    const uint32_t t1 = big ? umin(16u, n - 16u) : 0u, t2 = big ? umin(32u, n - 16u) : 0u,
+                   t3 = big ? umin(48u, n - 16u) : 0u;
+    if (off != 0u && off < n) {   // overlaps itself (off >= 16, n > 16): unit after unit
+        const uint8_t *s = L.win + ((uint32_t)ps - base);
+        lds_st16(w, lds16(s));
+        lds_st16(w + t1, lds16(s + t1));
+        lds_st16(w + t2, lds16(s + t2));
+        lds_st16(w + t3, lds16(s + t3));
+        return;
+    }
+    uint4 v0, v1, v2, v3;
+    if (!glb) {   // (offset 0: in-window bytes, zeroed below)
+        const uint8_t *s = L.win + ((uint32_t)ps - base);
+        v0 = lds16(s);
+        v1 = lds16(s + t1);
+        v2 = lds16(s + t2);
+        v3 = lds16(s + t3);
     } else {
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t q = q0 + j;
-            if (q >= lo && q < hi) {
-                L.ring[q & (kRing - 1)] = (uint8_t)(word >> (8 * j));
-                o8[j] = (uint8_t)(word >> (8 * j));
-            }
+        gcu8 *s = (DICT && ps < 0) ? D.dend + ps : (gcu8 *)D.dst + ps;
+        v0 = gload16_nt(s);
+        v1 = v2 = v3 = v0;
+        if (n > 16u) {
+            v1 = gload16_nt(s + t1);
+            v2 = gload16_nt(s + t2);
+            v3 = gload16_nt(s + t3);
         }
     }
+    if (off == 0u) v0 = v1 = v2 = v3 = make_uint4(0, 0, 0, 0);
+    if (big) {
+        lds_st16(w, v0);
+        lds_st16(w + t1, v1);
+        lds_st16(w + t2, v2);
+        lds_st16(w + t3, v3);
+    } else {
+        lds_put_small<true>(w, v0, n);
+    }
+}
+
+// Per-lane sequence of the batch: literal [o, m) from input ls, match [m, me) at offset off.
+struct Seq {
+    uint32_t o, m, me, ls, off;
+};
+
+// Produce output [S0, S1) of the batch in the window.  Round 1: every lane writes its
+// literal (short and staged) and its match when the sources lie before S0.  Then, while
+// something is pending: the first pending lane f's region starts at P, and everything
+// in [S0, P) is final; a coop item of f runs with the whole wave, otherwise every
+// pending lane whose sources end by P (f's always do) copies its match.
+template <bool DICT>
+__device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win &W, const Seq &q,
+                                             uint32_t S0, uint32_t S1, uint32_t &diag) {
+    const uint32_t base = W.base;
+    const uint32_t la = umax(q.o, S0), lb = umin(q.m, S1);
+    const uint32_t nl = lb > la ? lb - la : 0u;
+    const uint32_t lsrc = q.ls + (la - q.o);
+    const uint32_t ma = umax(q.m, S0), mb = umin(q.me, S1);
+    const uint32_t nm = mb > ma ? mb - ma : 0u;
+    const uint32_t off = q.off;
+    const int ps = (int)ma - (int)off;
+    // literal: lane path when short and staged
+    const uint32_t rs = lsrc - (uint32_t)D.s0;
+    const bool litL = nl != 0u && nl <= 16u && rs < (uint32_t)kStage && rs + nl <= (uint32_t)kStage;
+    bool litC = nl != 0u && !litL;
+    // match: lane path or coop; the end of its sources for the readiness test
+    const bool ovl = off != 0u && off < nm;
+    // (a match cut by a segment edge can be shorter than 4: the whole wave copies it)
+    bool lp, glb = false;
+    int pe;
+    if (off == 0u) {
+        lp = nm <= kLaneMax;
+        pe = -0x7FFFFFFF;
+    } else if (ovl) {
+        lp = off >= 16u && nm <= kLaneMax && ps >= (int)base;
+        pe = (int)ma;
+    } else {
+        pe = ps + (int)nm;
+        const bool inw = ps >= (int)base;
+        const bool ing = (!DICT || ps >= 0) && pe <= (int)W.gdone &&
+                         (nm >= 16u || ps + 16 <= D.cap);
+        const bool ind = DICT && ps + (int)umax(nm, 16u) <= 0;
+        lp = nm <= kLaneMax && (inw || ing || ind);
+        glb = !inw;
+    }
+    lp = lp && nm >= 4u;
+    const bool matC = nm != 0u && !lp;
+    bool mpend = nm != 0u;
+
+    // round 1
+    wave_sync();
+    if (litL) {
+        uint8_t *w = L.win + (la - base);
+        const uint4 v = lds16(L.stage + rs);
+        if (nl == 16u) lds_st16(w, v);
+        else lds_put_small<false>(w, v, nl);
+    }
+    const bool r1 = mpend && lp && pe <= (int)S0;
+    lane_match<DICT>(L, D, base, r1, ma, nm, off, glb);
+    mpend = mpend && !r1;
+    for (;;) {
+        wave_sync();
+        const uint64_t pm = wave_ballot(litC || mpend);
+        if (!pm) break;
+        diag += 1u;
+        const int f = __builtin_ctzll(pm);
+        if (lane_val(litC ? 1u : 0u, f)) {
+            coop_literal(L, D, base, lane_val(la, f), lane_val(nl, f), lane_val(lsrc, f));
+            if (D.lane == f) litC = false;
+            continue;
+        }
+        if (lane_val(matC ? 1u : 0u, f)) {
+            diag += 0x10000u;
+            coop_match<DICT>(L, D, base, lane_val(ma, f), lane_val(nm, f), lane_val(off, f));
+            if (D.lane == f) mpend = false;
+            continue;
+        }
+        const int P = (int)lane_val(ma, f);
+        const bool go = mpend && lp && pe <= P;
+        lane_match<DICT>(L, D, base, go, ma, nm, off, glb);
+        mpend = mpend && !go;
+    }
+}
+
+// Write window bytes [fl, F1) to dst: F1 = S1 rounded down to a 16-byte dst address
+// (the rest waits for the next flush), or S1 itself at the end of the block.
+__device__ __forceinline__ void flush(WaveLds &L, const Dec &D, Win &W, uint32_t S1, bool fin) {
+    const int lane = D.lane;
+    const uint32_t da = (uint32_t)(uintptr_t)D.dst & 15u;
+    const uint32_t F0 = W.fl;
+    const uint32_t sa = (S1 + da) & ~15u;
+    const uint32_t F1 = fin ? S1 : (sa > da ? sa - da : 0u);
+    if ((int)F1 <= (int)F0) return;
+    const uint32_t h = umin(((F0 + da + 15u) & ~15u) - da, F1);   // first 16-byte dst address
+    const uint32_t ta = (F1 + da) & ~15u;                          // last one
+    const uint32_t t = umax(ta > da ? ta - da : 0u, h);
+    const uint32_t base = W.base;
+    wave_sync();
+    if (lane < 16) {
+        const uint32_t x = F0 + (uint32_t)lane;
+        if (x < h) D.dst[x] = L.win[x - base];
+    } else if (lane < 32) {
+        const uint32_t x = t + (uint32_t)lane - 16u;
+        if (x < F1) D.dst[x] = L.win[x - base];
+    }
+    for (uint32_t c = h + 16u * (uint32_t)lane; c < t; c += 1024u)
+        gstore16(D.dst + c, lds16(L.win + (c - base)));
+    W.fl = F1;
+}
+
+// Slide the window to start at nb (a multiple of 16, <= S0 - kKeep): output [nb, S0)
+// moves to the window start; dst is drained, so everything below nb reads from dst.
+__device__ __forceinline__ void slide(WaveLds &L, const Dec &D, Win &W, uint32_t nb, uint32_t S0) {
+    const uint32_t from = nb - W.base, len = S0 - nb;   // len <= kKeep + 15
+    constexpr int kU = (int)((kKeep + 16u + 1023u) / 1024u);
+    uint4 v[kU];
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+        const uint32_t x = 16u * (uint32_t)D.lane + 1024u * (uint32_t)k;
+        if (x < len) v[k] = lds16(L.win + from + x);
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+        const uint32_t x = 16u * (uint32_t)D.lane + 1024u * (uint32_t)k;
+        if (x < len) lds_st16(L.win + x, v[k]);
+    }
+    wave_sync();
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    W.gdone = W.fl;
+    W.base = nb;
+}
+
+// Copy the batch's output [B0, B1) (nd descriptors) through the window to dst.
+template <bool DICT>
+__device__ __forceinline__ void copy_batch(WaveLds &L, const Dec &D, Win &W, int nd, uint32_t B0,
+                                           uint32_t B1, bool last, uint32_t &diag) {
+    const int lane = D.lane;
+    wave_sync();
+    const bool has = lane < nd;
+    const uint4 d = L.desc[has ? lane : 0];
+    const uint32_t nxt = lane + 1 < nd ? L.desc[lane + 1].y : B1;
+    Seq q;
+    q.o = has ? d.y : B1;
+    q.m = has ? d.y + d.z : B1;
+    q.me = has ? nxt : B1;
+    q.ls = d.x;
+    q.off = d.w;
+    for (uint32_t S0 = B0; S0 < B1;) {
+        if (B1 > W.base + kWinB && S0 >= W.base + kKeep + 16u) {
+            slide(L, D, W, (S0 - kKeep) & ~15u, S0);
+            diag += 1u << 24;
+        }
+        const uint32_t S1 = umin(B1, W.base + kWinB);
+        copy_segment<DICT>(L, D, W, q, S0, S1, diag);
+        flush(L, D, W, S1, last && S1 == B1);
+        S0 = S1;
+    }
+    if (last) flush(L, D, W, B1, true);
 }
 
 }  // namespace
@@ -555,7 +729,6 @@ lz4_decode_kernel(BlockArgs a) {
     STATS_DECL
     int P = 0;               // next token (wave-uniform)
     uint32_t op = 0;         // its output position
-    uint32_t gdone = 0;      // dst[0, gdone) stored and drained
     int result = 0;
     int st = ST_MORE;
     if (lane < 4) *(uint32_t *)&L.stage[kStage + 4 * lane] = 0u;  // over-read pad
@@ -574,14 +747,17 @@ lz4_decode_kernel(BlockArgs a) {
         return;
     }
 
-    // Output is copied in whole 256-byte steps: a batch copies up to the last step
-    // boundary its sequences reach and carries the descriptors of the unfinished
-    // step into the next batch (the last batch copies everything), so each step is
-    // produced once instead of once per batch that touches it.
-    uint32_t cstart = 0;     // output [0, cstart) copied
-    int nd = 0;              // descriptors in L.desc (carried ones first)
+    // Per batch: parse <= ~62 sequences into descriptors, then produce their output
+    // through the LDS window (copy_batch).  A failing sequence ends the block without
+    // copying its batch (the result is the error; dst bytes are unspecified then).
+    Win W;
+    W.base = 0;
+    W.fl = 0;
+    W.gdone = 0;
     while (st == ST_MORE) {
         // ---- PARSE one batch ----
+        const uint32_t B0 = op;
+        int nd = 0;
         bool restage = false;
         while (st == ST_MORE && nd <= kFlushAt) {
             if (P - D.s0 + kWinNeed > kStage) { restage = true; break; }
@@ -595,50 +771,14 @@ lz4_decode_kernel(BlockArgs a) {
         }
         STAT(0);
         if (st == ST_ERR) break;
-        // ---- COPY the batch's output [cstart, cend) ----
-        wave_sync();
-        const uint32_t bend = op;
-        const uint32_t d_out = lane < nd ? L.desc[lane].y : 0xFFFFFFFFu;   // ~0 past nd
-        // Copy through the last step boundary and carry the descriptors from the
-        // owner of that boundary on; with no new boundary, carry them all.  The
-        // last batch, or one that would carry too many, copies through its end.
-        uint32_t cend = bend & ~(uint32_t)(kStep - 1);
-        int keep = 0;
-        if (cend > cstart) keep = __popcll(wave_ballot(d_out <= cend)) - 1;
-        else cend = cstart;
-        const bool carry = st == ST_MORE && cend < bend && nd - keep <= kMaxCarry;
-        if (!carry) cend = bend;
-#ifdef APE_DEXP_NOCOPY
-        for (uint32_t base = cend; base < cend; base += kStep) {
-#else
-        for (uint32_t base = cstart & ~(uint32_t)(kStep - 1); base < cend; base += kStep) {
+        // ---- COPY the batch's output [B0, op) ----
+        uint32_t diag = 0;
+#ifndef APE_DEXP_NOCOPY   // diagnostic: instruction count of the parse alone (no output)
+        copy_batch<DICT>(L, D, W, nd, B0, op, st == ST_DONE, diag);
 #endif
-            const uint32_t lo = base > cstart ? base : cstart;
-            const uint32_t hi = base + kStep < cend ? base + kStep : cend;
-            if (lo - gdone > (uint32_t)(kRing / 2)) {
-                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                gdone = lo;
-            }
-            wave_sync();
-            uint32_t diag = 0;
-            copy_step<DICT>(L, D, base, lo, hi, gdone, nd, d_out, diag);
-            STAT_ADD(5, diag & 1u);          // steps with a period division
-            STAT_ADD(6, (diag >> 1) & 1u);   // steps with in-step sources
-            STAT_ADD(7, (diag >> 2) & 0x3FFFu);   // their resolution passes
-            STAT_ADD(8, diag >> 16);         // steps reading HBM history / literals
-            (void)diag;
-            STAT_ADD(3, 1);
-        }
-        cstart = cend;
-        if (carry) {   // desc[keep, nd) -> desc[0, nd - keep)
-            wave_sync();
-            const uint4 dv = L.desc[keep + (lane < nd - keep ? lane : 0)];
-            wave_sync();
-            if (lane < nd - keep) L.desc[lane] = dv;
-            nd -= keep;
-        } else {
-            nd = 0;
-        }
+        STAT_ADD(3, diag & 0xFFFFu);          // wave passes after round 1
+        STAT_ADD(5, (diag >> 16) & 0xFFu);    // coop matches
+        STAT_ADD(6, diag >> 24);              // window slides
         STAT(1);
         STAT_ADD(2, 1);
         if (restage && st == ST_MORE) {

@@ -13,9 +13,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ.setdefault("APE_LZ4_LIB", os.path.join(ROOT, "libapenetwork_amd", "libape_lz4_amd_stats.so"))
 sys.path.insert(0, ROOT)
 
-DEC = ["parse", "copy", "(batches)", "(steps)", "(restages)", "(division steps)",
-       "(in-step source steps)", "(resolution passes)", "(HBM-read steps)", "", "(blocks)", "", "",
-       "", "", ""]
+DEC = ["parse", "copy", "(batches)", "(passes after round 1)", "(restages)", "(coop matches)",
+       "(window slides)", "", "", "", "(blocks)", "", "", "", "", ""]
 ENC = ["W walk", "W publish", "E load", "W wait end", "W wait mid", "P F+M+H+L",
        "P wait mid", "P wait end", "(sequences)", "(batches)", "(steps x3 waves)",
        "(walker extensions)", "E store",
