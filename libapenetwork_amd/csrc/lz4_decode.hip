@@ -44,16 +44,19 @@ namespace {
 // its end, the window slides: the last kKeep bytes move to its start, and everything
 // older is read back from dst (flushed and drained by then).
 #ifndef APE_LZ4_DWIN
-#define APE_LZ4_DWIN 4096
+#define APE_LZ4_DWIN 2048
 #endif
 #ifndef APE_LZ4_DKEEP
-#define APE_LZ4_DKEEP 1024
+#define APE_LZ4_DKEEP 512
 #endif
 constexpr uint32_t kWinB = APE_LZ4_DWIN;   // output window bytes
 constexpr uint32_t kKeep = APE_LZ4_DKEEP;  // history kept when the window slides
 static_assert(kKeep >= 64 && kKeep % 16 == 0 && kWinB >= kKeep + 1024 && kWinB % 16 == 0,
               "output window");
-constexpr int kStage = 2304;     // staged compressed bytes per batch (9 dwords/lane)
+#ifndef APE_LZ4_DSTAGE
+#define APE_LZ4_DSTAGE 2304
+#endif
+constexpr int kStage = APE_LZ4_DSTAGE;   // staged compressed bytes (a multiple of 256)
 constexpr int kWinNeed = 84;     // a parse window reads up to P + 63 + 21
 constexpr int kMaxDesc = 64;     // descriptors per batch
 constexpr int kFlushAt = 40;     // copy once a batch holds more than this (window adds <= 22)
@@ -509,14 +512,16 @@ struct Seq {
     uint32_t o, m, me, ls, off;
 };
 
-// Produce output [S0, S1) of the batch in the window.  Round 1: every lane writes its
-// literal (short and staged) and its match when the sources lie before S0.  Then, while
-// something is pending: the first pending lane f's region starts at P, and everything
-// in [S0, P) is final; a coop item of f runs with the whole wave, otherwise every
-// pending lane whose sources end by P (f's always do) copies its match.
+// Produce output [S0, S1) of the batch in the window.  Literals first (a lane each when
+// short and staged, the whole wave for the others), then round 1: every match whose
+// sources lie before S0.  The remaining matches read output of this segment: each finds
+// the sequences owning its source range (binary search over the sequence starts) and runs
+// in the first pass after all of them are done.  A pass with nothing ready means the first
+// pending sequence is a whole-wave item (everything before it is done): it runs then.
 template <bool DICT>
 __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win &W, const Seq &q,
                                              uint32_t S0, uint32_t S1, uint32_t &diag) {
+    const int lane = D.lane;
     const uint32_t base = W.base;
     const uint32_t la = umax(q.o, S0), lb = umin(q.m, S1);
     const uint32_t nl = lb > la ? lb - la : 0u;
@@ -528,32 +533,26 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
     // literal: lane path when short and staged
     const uint32_t rs = lsrc - (uint32_t)D.s0;
     const bool litL = nl != 0u && nl <= 16u && rs < (uint32_t)kStage && rs + nl <= (uint32_t)kStage;
-    bool litC = nl != 0u && !litL;
-    // match: lane path or coop; the end of its sources for the readiness test
+    // match: lane path (window / dst history / dictionary sources, or a self-overlap with
+    // offset >= 16 inside the window; a match cut by a segment edge can be shorter than 4)
+    // or the whole wave; pe = end of the sources it needs from this segment
     const bool ovl = off != 0u && off < nm;
-    // (a match cut by a segment edge can be shorter than 4: the whole wave copies it)
-    bool lp, glb = false;
-    int pe;
-    if (off == 0u) {
-        lp = nm <= kLaneMax;
-        pe = -0x7FFFFFFF;
-    } else if (ovl) {
-        lp = off >= 16u && nm <= kLaneMax && ps >= (int)base;
-        pe = (int)ma;
-    } else {
-        pe = ps + (int)nm;
-        const bool inw = ps >= (int)base;
-        const bool ing = (!DICT || ps >= 0) && pe <= (int)W.gdone &&
-                         (nm >= 16u || ps + 16 <= D.cap);
-        const bool ind = DICT && ps + (int)umax(nm, 16u) <= 0;
-        lp = nm <= kLaneMax && (inw || ing || ind);
-        glb = !inw;
-    }
-    lp = lp && nm >= 4u;
-    const bool matC = nm != 0u && !lp;
+    const int pe0 = ps + (int)nm;
+    const bool inw = ps >= (int)base;
+    const bool ing = (!DICT || ps >= 0) && pe0 <= (int)W.gdone && (nm >= 16u || ps + 16 <= D.cap);
+    const bool ind = DICT && ps + (int)umax(nm, 16u) <= 0;
+    const bool lp_n = inw || ing || ind;
+    const bool lp_o = off >= 16u && inw;
+    const bool lp = nm >= 4u && nm <= kLaneMax && (off == 0u || (ovl ? lp_o : lp_n));
+    const bool glb = off != 0u && !inw;
+    const int pe = off == 0u ? -0x7FFFFFFF : (ovl ? (int)ma : pe0);
     bool mpend = nm != 0u;
 
-    // round 1
+    // literals
+    for (uint64_t lc = wave_ballot(nl != 0u && !litL); lc; lc &= lc - 1ull) {
+        const int f = __builtin_ctzll(lc);
+        coop_literal(L, D, base, lane_val(la, f), lane_val(nl, f), lane_val(lsrc, f));
+    }
     wave_sync();
     if (litL) {
         uint8_t *w = L.win + (la - base);
@@ -561,30 +560,45 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
         if (nl == 16u) lds_st16(w, v);
         else lds_put_small<false>(w, v, nl);
     }
+    // round 1
     const bool r1 = mpend && lp && pe <= (int)S0;
     lane_match<DICT>(L, D, base, r1, ma, nm, off, glb);
     mpend = mpend && !r1;
+    uint64_t pm = wave_ballot(mpend);
+    if (!pm) return;
+    // sequences owning [max(ps, S0), pe): k0 = owner(first byte), k1 = owner(last byte),
+    // by binary search over the sequence starts (lanes past the batch hold B1)
+    const uint32_t x0 = (uint32_t)(ps > (int)S0 ? ps : (int)S0), x1 = (uint32_t)(pe - 1);
+    uint32_t k0 = 0, k1 = 0;
+#pragma unroll
+    for (uint32_t st = 32; st >= 1; st >>= 1) {
+        const uint32_t c0 = k0 + st, c1 = k1 + st;
+        const uint32_t v0 = bperm(q.o, c0), v1 = bperm(q.o, c1);
+        k0 = v0 <= x0 ? c0 : k0;
+        k1 = v1 <= x1 ? c1 : k1;
+    }
+    k1 = umin(k1, (uint32_t)lane - 1u);   // (its own literal is written; lane 0 has no needs)
+    const uint64_t need = (mpend && lane > 0 && k0 <= k1)
+                              ? (((2ull << k1) - 1ull) & ~((1ull << k0) - 1ull)) : 0ull;
+    uint64_t done = ~pm;
+    wave_sync();
     for (;;) {
-        wave_sync();
-        const uint64_t pm = wave_ballot(litC || mpend);
-        if (!pm) break;
         diag += 1u;
-        const int f = __builtin_ctzll(pm);
-        if (lane_val(litC ? 1u : 0u, f)) {
-            coop_literal(L, D, base, lane_val(la, f), lane_val(nl, f), lane_val(lsrc, f));
-            if (D.lane == f) litC = false;
-            continue;
-        }
-        if (lane_val(matC ? 1u : 0u, f)) {
+        const bool go = mpend && lp && (need & ~done) == 0ull;
+        const uint64_t gm = wave_ballot(go);
+        if (gm) {
+            lane_match<DICT>(L, D, base, go, ma, nm, off, glb);
+            mpend = mpend && !go;
+            done |= gm;
+        } else {   // the first pending sequence is a whole-wave item, and its sources are done
+            const int f = __builtin_ctzll(pm & ~done);
             diag += 0x10000u;
             coop_match<DICT>(L, D, base, lane_val(ma, f), lane_val(nm, f), lane_val(off, f));
-            if (D.lane == f) mpend = false;
-            continue;
+            if (lane == f) mpend = false;
+            done |= 1ull << f;
         }
-        const int P = (int)lane_val(ma, f);
-        const bool go = mpend && lp && pe <= P;
-        lane_match<DICT>(L, D, base, go, ma, nm, off, glb);
-        mpend = mpend && !go;
+        if (!(pm & ~done)) break;
+        wave_sync();
     }
 }
 
