@@ -58,8 +58,8 @@ static_assert(kKeep >= 64 && kKeep % 16 == 0 && kWinB >= kKeep + 1024 && kWinB %
 #endif
 constexpr int kStage = APE_LZ4_DSTAGE;   // staged compressed bytes (a multiple of 256)
 constexpr int kWinNeed = 84;     // a parse window reads up to P + 63 + 21
-constexpr int kMaxDesc = 64;     // descriptors per batch
-constexpr int kFlushAt = 40;     // copy once a batch holds more than this (window adds <= 22)
+constexpr int kBatch = 64;       // descriptors per copy batch (one per lane)
+constexpr int kMaxDesc = kBatch + 48;   // held before a copy: < 64, + <= 44 per parse step, + 1
 constexpr uint32_t kLaneMax = 64;  // longest match one lane copies (4 x 16 bytes)
 
 struct __attribute__((aligned(16))) WaveLds {
@@ -285,29 +285,23 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
     return z;
 }
 
-// One speculative window at P (P - s0 + kWinNeed <= kStage): appends the chain's
-// descriptors.  Returns ST_MORE with P advanced (to the next token, or to a complex
-// token when `cplx`), or ST_DONE / ST_ERR with `res`.
-//
-// Every lane parses "the sequence at P + lane" and its successor (hop).  The true
-// chain from P is found by binary lifting instead of a serial walk: J_k = hop^(2^k)
-// (four ds_bpermute rounds), and lane t composes them by the bits of t into the
-// position of the chain's t-th sequence (a window holds <= 22: each sequence takes
-// >= 3 input bytes).  Lane t then re-reads its member from the staged bytes, so the
-// members arrive compacted and in order.
-template <bool PARTIAL, bool DICT, bool FASTD = false>
-__device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int &nd, int &res,
-                            bool &cplx) {
-    const int lane = D.lane;
-    // a final / failing sequence ends the chain (kHopTerm), a complex token ends it
-    // before itself (kHopCplx); every exit value is >= 64 and absorbs
-    constexpr uint32_t kHopTerm = 0x80u, kHopCplx = 0xC0u;
+// The chain of sequences from window position 0 of a window at P: every lane parses
+// "the sequence at P + lane" and its successor (hop).  The true chain is found by binary
+// lifting instead of a serial walk: J_k = hop^(2^k) (four ds_bpermute rounds), and lane t
+// composes them by the bits of t into pos = the window position of the chain's t-th
+// sequence (a window holds <= 22: each sequence takes >= 3 input bytes).  cnt members
+// (lanes [0, cnt)); X = the chain's exit (next token position >= 64, or kHopTerm after a
+// final / failing sequence, kHopCplx before a complex token); lastp = the last member.
+constexpr uint32_t kHopTerm = 0x80u, kHopCplx = 0xC0u;
+template <bool FASTD>
+__device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, uint32_t &pos,
+                                         int &cnt, uint32_t &X, uint32_t &lastp) {
     uint32_t hop;
     {
-        const Spec z = spec_at<FASTD>(L, D, P, (uint32_t)lane);
+        const Spec z = spec_at<FASTD>(L, D, P, (uint32_t)D.lane);
         hop = z.cx ? kHopCplx : ((z.fin_in || z.mlerr) ? kHopTerm : (uint32_t)(z.q - P));
     }
-    auto jump = [](uint32_t J, uint32_t idx) {
+    auto jump = [](uint32_t J, uint32_t idx) {   // exit values (>= 64) absorb
         const uint32_t g = bperm(J, idx & 63u);
         return idx < 64u ? g : idx;
     };
@@ -315,29 +309,59 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const uint32_t J2 = jump(J1, J1);
     const uint32_t J3 = jump(J2, J2);
     const uint32_t J4 = jump(J3, J3);
+    const uint32_t t = (uint32_t)D.lane;
+    uint32_t p = (t & 1u) ? lane_val(hop, 0) : 0u;
+    const uint32_t p2 = jump(J1, p);
+    p = (t & 2u) ? p2 : p;
+    const uint32_t p4 = jump(J2, p);
+    p = (t & 4u) ? p4 : p;
+    const uint32_t p8 = jump(J3, p);
+    p = (t & 8u) ? p8 : p;
+    const uint32_t p16 = jump(J4, p);
+    p = (t & 16u) ? p16 : p;
+    pos = t < 32u ? p : kHopTerm;
+    cnt = __popcll(wave_ballot(pos < 64u));
+    X = lane_val(pos, cnt);
+    lastp = lane_val(pos, cnt - 1);
+}
+
+// Up to two speculative windows (P, then where the first one's chain leaves it, if that
+// is staged) and one pass over their members: appends the descriptors (<= 44).  Returns
+// ST_MORE with P advanced (to the next token, or to a complex token when `cplx`), or
+// ST_DONE / ST_ERR with `res`.  Members are lanes [0, nm) in chain order: lane t re-reads
+// its sequence from the staged bytes.
+template <bool PARTIAL, bool DICT, bool FASTD = false>
+__device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int &nd, int &res,
+                            bool &cplx) {
+    const int lane = D.lane;
     const uint32_t t = (uint32_t)lane;
-    uint32_t pos = (t & 1u) ? lane_val(hop, 0) : 0u;
-    {
-        const uint32_t p2 = jump(J1, pos);
-        pos = (t & 2u) ? p2 : pos;
-        const uint32_t p4 = jump(J2, pos);
-        pos = (t & 4u) ? p4 : pos;
-        const uint32_t p8 = jump(J3, pos);
-        pos = (t & 8u) ? p8 : pos;
-        const uint32_t p16 = jump(J4, pos);
-        pos = (t & 16u) ? p16 : pos;
+    uint32_t posA, XA, lastA;
+    int cntA;
+    chain_at<FASTD>(L, D, P, posA, cntA, XA, lastA);
+    const bool cplxA = XA == kHopCplx;
+    const int nmA = cplxA ? cntA - 1 : cntA;   // the complex token is not a member
+    const int PB = P + (int)XA;
+    const bool two = XA < kHopTerm && PB - D.s0 + kWinNeed <= kStage;
+    int nmB = 0, Pn;
+    uint32_t posB = 0;
+    if (two) {
+        uint32_t XB, lastB;
+        int cntB;
+        chain_at<FASTD>(L, D, PB, posB, cntB, XB, lastB);
+        cplx = XB == kHopCplx;
+        nmB = cplx ? cntB - 1 : cntB;
+        Pn = PB + (int)(XB >= kHopTerm ? lastB : XB);   // (not past a final token)
+    } else {
+        cplx = cplxA;
+        Pn = P + (int)(XA >= kHopTerm ? lastA : XA);
     }
-    pos = t < 32u ? pos : kHopTerm;
-    const int cnt = __popcll(wave_ballot(pos < 64u));   // chain members: lanes [0, cnt)
-    const uint32_t X = lane_val(pos, cnt);               // the chain's exit
-    const uint32_t lastp = lane_val(pos, cnt - 1);
-    cplx = X == kHopCplx;
-    const int nm = cplx ? cnt - 1 : cnt;                 // the complex token is not a member
-    const uint32_t c = X >= kHopTerm ? lastp : X;        // (P is not advanced past a final token)
-    const uint64_t M = (1ull << nm) - 1ull;              // nm <= 22
+    const uint32_t pB = bperm(posB, (t - (uint32_t)nmA) & 63u);
+    const int nm = nmA + nmB;
+    const uint64_t M = (1ull << nm) - 1ull;   // nm <= 44
+    const bool mem = (int)t < nm;
+    const uint32_t pos = (int)t < nmA ? posA : (uint32_t)(PB - P) + pB;   // relative to P
 
     // member t = the sequence at P + pos, re-read from the staged bytes
-    const bool mem = (int)t < nm;
     const Spec z = spec_at<FASTD>(L, D, P, mem ? pos : 0u);
     const uint32_t lit = z.lit, ml = z.ml, off = z.off;
     const int ipl = z.ipl, ipo = z.ipo, q = z.q;
@@ -377,7 +401,7 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
         res = (int)lane_val((uint32_t)rv, T);
         const bool tbad = lane_val(bad ? 1u : 0u, T) != 0u;
         // members before T (error) or up to T (final literals)
-        emit = tbad ? ((1ull << T) - 1ull) : ((2ull << T) - 1ull);   // T <= 21
+        emit = tbad ? ((1ull << T) - 1ull) : ((2ull << T) - 1ull);   // T <= 43
         st = tbad ? ST_ERR : ST_DONE;
         cplx = false;
     }
@@ -391,7 +415,7 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
             op = lane_val(opl + (fin ? lit : ob), ne - 1);
         }
     }
-    if (st == ST_MORE) P += (int)c;
+    if (st == ST_MORE) P = Pn;
     return st;
 }
 
@@ -761,19 +785,20 @@ lz4_decode_kernel(BlockArgs a) {
         return;
     }
 
-    // Per batch: parse <= ~62 sequences into descriptors, then produce their output
-    // through the LDS window (copy_batch).  A failing sequence ends the block without
-    // copying its batch (the result is the error; dst bytes are unspecified then).
+    // Per batch: parse until >= 64 descriptors are held (a parse step adds <= 44), then
+    // produce the output of the first 64 through the LDS window (copy_batch) and carry
+    // the rest.  A failing sequence ends the block without copying its batch (the result
+    // is the error; dst bytes are unspecified then).
     Win W;
     W.base = 0;
     W.fl = 0;
     W.gdone = 0;
-    while (st == ST_MORE) {
-        // ---- PARSE one batch ----
-        const uint32_t B0 = op;
-        int nd = 0;
+    int nd = 0;              // descriptors held (carried ones first)
+    uint32_t cst = 0;        // output position of desc[0]
+    for (;;) {
+        // ---- PARSE ----
         bool restage = false;
-        while (st == ST_MORE && nd <= kFlushAt) {
+        while (st == ST_MORE && nd < kBatch) {
             if (P - D.s0 + kWinNeed > kStage) { restage = true; break; }
             bool cplx;
             st = parse_window<PARTIAL, DICT, FASTD>(L, D, P, op, nd, result, cplx);
@@ -785,17 +810,33 @@ lz4_decode_kernel(BlockArgs a) {
         }
         STAT(0);
         if (st == ST_ERR) break;
-        // ---- COPY the batch's output [B0, op) ----
-        uint32_t diag = 0;
+        // ---- COPY: batches of <= 64 descriptors; all of them before a restage (their
+        // literals are staged) or at the end ----
+        do {
+            const int nc = nd < kBatch ? nd : kBatch;
+            wave_sync();
+            const uint32_t B1 = nc < nd ? (uint32_t)__builtin_amdgcn_readfirstlane(L.desc[nc].y) : op;
+            const bool last = st == ST_DONE && nc == nd;
+            uint32_t diag = 0;
 #ifndef APE_DEXP_NOCOPY   // diagnostic: instruction count of the parse alone (no output)
-        copy_batch<DICT>(L, D, W, nd, B0, op, st == ST_DONE, diag);
+            copy_batch<DICT>(L, D, W, nc, cst, B1, last, diag);
 #endif
-        STAT_ADD(3, diag & 0xFFFFu);          // wave passes after round 1
-        STAT_ADD(5, (diag >> 16) & 0xFFu);    // coop matches
-        STAT_ADD(6, diag >> 24);              // window slides
+            STAT_ADD(3, diag & 0xFFFFu);          // wave passes after round 1
+            STAT_ADD(5, (diag >> 16) & 0xFFu);    // coop matches
+            STAT_ADD(6, diag >> 24);              // window slides
+            STAT_ADD(2, 1);
+            cst = B1;
+            if (nc < nd) {   // carry desc[nc, nd) -> desc[0, nd - nc)
+                wave_sync();
+                const uint4 dv = L.desc[nc + (lane < nd - nc ? lane : 0)];
+                wave_sync();
+                if (lane < nd - nc) L.desc[lane] = dv;
+            }
+            nd -= nc;
+        } while (nd > 0 && (restage || st != ST_MORE));
         STAT(1);
-        STAT_ADD(2, 1);
-        if (restage && st == ST_MORE) {
+        if (st != ST_MORE) break;
+        if (restage) {
             wave_sync();
             D.s0 = stage_base(D.src, P);
             stage_load(L, D.src, D.csize, D.s0, lane);
