@@ -856,7 +856,11 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         WalkOut O;
         __syncthreads();
         for (int s = k0; s < nsteps; s++) {
+#ifdef APE_EXP_NOWALK
+            const bool work = false;   // diagnostic: instruction count without the walker
+#else
             const bool work = s >= k0 + 1 && s <= nch;
+#endif
             if (work) walk_chain<ACC>(S, B, s - 1, lane, W, O);
             STAT(0);
             __syncthreads();
