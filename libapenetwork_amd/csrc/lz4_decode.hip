@@ -296,14 +296,16 @@ constexpr uint32_t kHopTerm = 0x80u, kHopCplx = 0xC0u;
 template <bool FASTD>
 __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, uint32_t &pos,
                                          int &cnt, uint32_t &X, uint32_t &lastp) {
+    // hop and the J_k hold window positions x 4: ds_bpermute's byte address (it uses
+    // address bits [7:2] only), so an exit (>= 64, i.e. >= 256 here) needs no mask
     uint32_t hop;
     {
         const Spec z = spec_at<FASTD>(L, D, P, (uint32_t)D.lane);
-        hop = z.cx ? kHopCplx : ((z.fin_in || z.mlerr) ? kHopTerm : (uint32_t)(z.q - P));
+        hop = 4u * (z.cx ? kHopCplx : ((z.fin_in || z.mlerr) ? kHopTerm : (uint32_t)(z.q - P)));
     }
-    auto jump = [](uint32_t J, uint32_t idx) {   // exit values (>= 64) absorb
-        const uint32_t g = bperm(J, idx & 63u);
-        return idx < 64u ? g : idx;
+    auto jump = [](uint32_t J, uint32_t a) {   // exit values absorb
+        const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)J);
+        return a < 256u ? g : a;
     };
     const uint32_t J1 = jump(hop, hop);
     const uint32_t J2 = jump(J1, J1);
@@ -319,6 +321,7 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
     p = (t & 8u) ? p8 : p;
     const uint32_t p16 = jump(J4, p);
     p = (t & 16u) ? p16 : p;
+    p >>= 2;
     pos = t < 32u ? p : kHopTerm;
     cnt = __popcll(wave_ballot(pos < 64u));
     X = lane_val(pos, cnt);

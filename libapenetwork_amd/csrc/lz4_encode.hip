@@ -435,7 +435,11 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     uint32_t len = R.len;
     bool trunc = false;
+#ifdef APE_EXP_C2ANY
+    if (wave_any(R.trunc1)) {   // no lane reached C1's cap: nothing to finish
+#else
     {   // unconditional for the same reason as in C1
+#endif
         uint32_t O[8];
         ring32(S, p + R.base, O);                // own bytes p+base .. p+base+32
         const uint32_t ext = umin(first_diff_bit<0, 8>(O, E) >> 3, 32u);
