@@ -67,8 +67,13 @@ namespace {
 #endif
 constexpr int kHLog = APE_LZ4_HLOG;
 constexpr int kHSize = 1 << kHLog;
-constexpr uint32_t kEagerLen = 28;   // match bytes measured by the producer (T candidate)
+constexpr uint32_t kEagerLen = 20;   // match bytes measured by C1 (T candidate)
 constexpr uint32_t kEagerL = 12;     // ... for the in-chunk candidate L
+// Stage 2 (C2) measures only the candidates C1 left truncated (~8 % of the lanes on App.
+// C data), compacted into groups of 4 lanes that compare 16 bytes each: 64 more bytes
+// per candidate, 16 candidates per pass (a second pass is rare).
+constexpr uint32_t kExt2 = 64;
+constexpr uint32_t kGroups = 16;
 #ifndef APE_LZ4_ERING
 #define APE_LZ4_ERING 1024
 #endif
@@ -216,8 +221,9 @@ __device__ __forceinline__ uint32_t ffbh(uint32_t d) {
 
 // first differing bit of dwords A[K0..K1) vs B (bit index from A[K0]'s bit 0), or
 // 0xFFFFFFFF: ffbl + saturating add + min3 per dword, no compares or selects
-template <int K0, int K1>
-__device__ __forceinline__ uint32_t first_diff_bit(const uint32_t (&A)[8], const uint32_t (&B)[8]) {
+template <int K0, int K1, int NA, int NB>
+__device__ __forceinline__ uint32_t first_diff_bit(const uint32_t (&A)[NA], const uint32_t (&B)[NB]) {
+    static_assert(K1 <= NA && K1 <= NB, "dwords");
     uint32_t m = ffbl(A[K0] ^ B[K0]);
 #pragma unroll
     for (int k = K0 + 1; k < K1; k++)
@@ -226,8 +232,8 @@ __device__ __forceinline__ uint32_t first_diff_bit(const uint32_t (&A)[8], const
 }
 
 // common length of X and Y from byte 4 (dword 1) on, up to kEagerLen
-__device__ __forceinline__ uint32_t eager(const uint32_t (&X)[8], const uint32_t (&Y)[8]) {
-    return umin((first_diff_bit<2, 8>(X, Y) >> 3) + 4u, kEagerLen);
+__device__ __forceinline__ uint32_t eager(const uint32_t (&X)[6], const uint32_t (&Y)[6]) {
+    return umin((first_diff_bit<2, 6>(X, Y) >> 3) + 4u, kEagerLen);
 }
 
 // bytes equal just before the match (in[p-1] == in[c-1], ...), 0..4
@@ -256,21 +262,68 @@ __device__ __forceinline__ void put_len(gu8 *o, uint32_t v) {
     o[k] = (uint8_t)v;
 }
 
-// 4 input bytes at x from the ring
-__device__ __forceinline__ uint32_t ring4(const EncLds &S, uint32_t x) {
-    const uint32_t *r = S.ring + ((x >> 2) & (kRingE / 4 - 1));
-    return __builtin_amdgcn_alignbyte(r[1], r[0], x & 3u);
+// 16 / 8 input bytes at x from the ring (the mirrored tail keeps a read that starts in
+// the last 64 bytes contiguous): aligned dword reads + v_alignbyte.  (Measured against
+// single unaligned ds_read_b128 / _b64, APE_EXP_UNALIGNED_RING: 12.5 vs 11.3 ms per 16384
+// blocks -- fewer VALU instructions, but a 1-byte lane stride makes the unaligned reads
+// slow.)
+#ifdef APE_EXP_UNALIGNED_RING
+typedef uint32_t l32x4 __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t l32x2 __attribute__((ext_vector_type(2), aligned(1)));
+__device__ __forceinline__ uint4 ring16(const EncLds &S, uint32_t x) {
+    const l32x4 v = *(const l32x4 *)((const uint8_t *)S.ring + (x & (kRingE - 1)));
+    return make_uint4(v.x, v.y, v.z, v.w);
 }
-
-// 32 input bytes at x from the ring
-__device__ __forceinline__ void ring32(const EncLds &S, uint32_t x, uint32_t (&O)[8]) {
+__device__ __forceinline__ uint2 ring8(const EncLds &S, uint32_t x) {
+    const l32x2 v = *(const l32x2 *)((const uint8_t *)S.ring + (x & (kRingE - 1)));
+    return make_uint2(v.x, v.y);
+}
+#else
+__device__ __forceinline__ uint4 ring16(const EncLds &S, uint32_t x) {
     const uint32_t *r = S.ring + ((x >> 2) & (kRingE / 4 - 1));
     const uint32_t sh = x & 3u;
-    uint32_t W[9];
+    const uint32_t w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3], w4 = r[4];
+    return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                      __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+}
+__device__ __forceinline__ uint2 ring8(const EncLds &S, uint32_t x) {
+    const uint32_t *r = S.ring + ((x >> 2) & (kRingE / 4 - 1));
+    const uint32_t sh = x & 3u;
+    const uint32_t w0 = r[0], w1 = r[1], w2 = r[2];
+    return make_uint2(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh));
+}
+#endif
+
+// NW dwords in[pos, pos + 4 NW) (NW = 4 or 6).  fast: the window lies inside [0, n)
+// (vector loads); otherwise byte loads, bytes outside [0, n) read as 0 (the edge steps
+// and blocks below kSmall only).
+template <int NW>
+__device__ __forceinline__ void loadv(gcu8 *in, uint32_t un, uint32_t pos, uint32_t (&X)[NW],
+                                      bool fast) {
+    static_assert(NW == 4 || NW == 6, "loadv");
+    if (fast) {
+        const uint4 a = gload16(in + pos);
+        X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w;
+        if (NW == 6) {
+            const uint2 b = gload8(in + pos + 16u);
+            X[4] = b.x; X[5] = b.y;
+        }
+        return;
+    }
 #pragma unroll
-    for (int k = 0; k < 9; k++) W[k] = r[k];
+    for (int k = 0; k < NW; k++) X[k] = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) O[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
+    for (uint32_t t = 0; t < 4u * NW; t++)
+        if (pos + t < un) X[t >> 2] |= (uint32_t)in[pos + t] << (8 * (t & 3));
+}
+
+// lane l receives v of lane idx (idx mod 64)
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t idx) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(idx << 2), (int)v);
+}
+// rank of this lane among the set lanes of m below it
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 // Copy in[a, a+len) to dst[o, o+len) with the whole wave (16 bytes per lane per step).
@@ -302,6 +355,7 @@ struct Blk {
 // ---------------- producer ----------------
 struct Part {                        // C1 result of one chunk, finished by C2
     uint32_t len, c, bk, lim, h, base;   // base: bytes C1 measured (kEagerLen / kEagerL)
+    uint32_t rank, ntr, eo;          // stage-2 queue rank, queue size, own bytes of the group
     bool has, hashable, trunc1;
 };
 
@@ -310,8 +364,8 @@ struct Part {                        // C1 result of one chunk, finished by C2
 // C1 for C2.
 struct PSet {
     uint32_t X[2];                   // own bytes in[p, p+8) of the chunk B works on next
-    uint32_t Y[8];                   // T-candidate bytes
-    uint32_t E[8];                   // second-stage candidate bytes
+    uint32_t Y[6];                   // T-candidate bytes in[T-4, T+20)
+    uint32_t E[4];                   // stage-2 candidate bytes of this lane's group
     uint32_t cT, jL, h;
     Part q;
 };
@@ -332,22 +386,22 @@ __device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_
         if (pos + t < B.un) X[t >> 2] |= (uint32_t)B.in[pos + t] << (8 * (t & 3));
 }
 
-// T candidate bytes of chunk k (issued one step before C1 consumes them).  Candidates
-// below position 4 are skipped: their 4 bytes of backward context would start before
-// the block and need the slow edge path (never-written slots read as 0).
+// T candidate bytes in[T-4, T+20) of chunk k (issued one step before C1 consumes them).
+// Candidates below position 4 are skipped: their 4 bytes of backward context would start
+// before the block (never-written slots read as 0).
 template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_fetch_t(const Blk &B, int k, int lane, uint32_t cT,
-                                             uint32_t (&Y)[8]) {
+                                             uint32_t (&Y)[6]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const bool tryT = k < B.nch && cT < p && cT >= 4u;
-    load32<SMALL>(B.in, B.n, tryT ? (int)cT - 4 : 0, Y, FAST || 64 * k + 91 <= B.n);
+    loadv<6>(B.in, B.un, tryT ? cT - 4u : 0u, Y, FAST || (!SMALL && 64 * k + 83 <= B.n));
 }
 
 // B(k): hash, table + in-chunk candidates, T fetch issue, ring copy
 template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int lane,
                                             const uint32_t (&X)[2], uint32_t &cT, uint32_t &jL,
-                                            uint32_t &h, uint32_t (&Y)[8]) {
+                                            uint32_t &h, uint32_t (&Y)[6]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const bool live = k < B.nch;
     const bool hashable = live && p + 5u <= B.un;
@@ -362,49 +416,91 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
         wave_sync();
         if (hashable) S.scr[hs] = 0xFFFFFFFFu;
     }
-    // ring copy of this chunk (own bytes for C1, second stage, match_end - 2,
-    // literals); zero past the block end
+    // ring copy of this chunk (own bytes for C1, stage 2, match_end - 2, literals);
+    // zero past the block end
     if (live) {
         const uint8_t by = (uint8_t)X[0];
         ((uint8_t *)S.ring)[p & (kRingE - 1)] = by;
         if (((64u * (uint32_t)k) & (kRingE - 1)) == 0u) ((uint8_t *)S.ring)[kRingE + lane] = by;
     }
-    // T candidate bytes (issued now, consumed one step later).  Candidates below
-    // position 4 are skipped: their 4 bytes of backward context would start before
-    // the block and need the slow edge path (never-written slots read as 0).
     if (!kWin) prod_fetch_t<SMALL, FAST>(B, k, lane, cT, Y);
 }
 
-// C1(k): verify / measure 28 bytes / pick; issue the second-stage load
+// Stage-2 group of this lane for the truncated lanes of ranks [first, first + kGroups):
+// the lane of rank first + g pushes its continuation points to lane 4g (ds_permute, a
+// forward permute; the other lanes push to odd lanes, never read), and the quad
+// broadcasts them; lane 4g + i then compares the 16 bytes at offset 16 i.  Returns
+// whether the group has an entry; cb / eo = candidate / own position of those bytes.
+__device__ __forceinline__ bool stage2_group(const Part &R, int lane, uint32_t first, uint32_t p,
+                                             uint32_t &cb, uint32_t &eo) {
+    const uint32_t r = R.rank - first, i16 = 16u * ((uint32_t)lane & 3u);
+    const bool push = R.trunc1 && r < kGroups;
+    const int tgt = (int)((push ? 4u * r : ((uint32_t)lane | 1u)) << 2);
+    cb = dpp<0x00>(0u, (uint32_t)__builtin_amdgcn_ds_permute(tgt, (int)(R.c + R.base))) + i16;
+    eo = dpp<0x00>(0u, (uint32_t)__builtin_amdgcn_ds_permute(tgt, (int)(p + R.base))) + i16;
+    return first + ((uint32_t)lane >> 2) < R.ntr;
+}
+
+// Stage-2 result of entry `first + g` (all four lanes of group g): bytes equal from the
+// continuation point, 0..kExt2
+__device__ __forceinline__ uint32_t stage2_len(const EncLds &S, int lane, uint32_t eo,
+                                               const uint32_t (&E)[4]) {
+    const uint4 o = ring16(S, eo);
+    const uint32_t O[4] = {o.x, o.y, o.z, o.w};
+    uint32_t d = __builtin_elementwise_add_sat(first_diff_bit<0, 4>(O, E),
+                                               128u * ((uint32_t)lane & 3u));
+    d = umin(d, dpp<0xB1>(0u, d));   // quad_perm [1,0,3,2]
+    d = umin(d, dpp<0x4E>(0u, d));   // quad_perm [2,3,0,1]
+    return umin(d >> 3, kExt2);
+}
+
+// C1(k): verify / measure to 20 bytes / pick; queue the truncated candidates and issue
+// the stage-2 loads of the first kGroups of them
 template <bool SMALL, bool FAST = false>
-__device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int k, int lane,
-                                             const uint32_t (&Y)[8], uint32_t cT, uint32_t jL,
-                                             uint32_t h, Part &R, uint32_t (&E)[8]) {
+__device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int lane,
+                                             const uint32_t (&Y)[6], uint32_t cT, uint32_t jL,
+                                             uint32_t h, Part &R) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-    uint32_t X[8];
-    ring32(S, p - 4u, X);            // own bytes in[p-4, p+28) (ring tail = 0 before 0)
-    uint32_t Yw[8];
+    uint32_t X[6];                   // own bytes in[p-4, p+20) (ring tail = 0 before 0)
+#ifdef APE_EXP_UNALIGNED_RING
+    {
+        const uint4 a = ring16(S, p - 4u);
+        const uint2 b = ring8(S, p + 12u);
+        X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w; X[4] = b.x; X[5] = b.y;
+    }
+#else
+    {   // 7 aligned dwords, 6 alignbytes
+        const uint32_t *r = S.ring + (((p - 4u) >> 2) & (kRingE / 4 - 1));
+        const uint32_t sh = p & 3u;
+        uint32_t W[7];
+#pragma unroll
+        for (int t = 0; t < 7; t++) W[t] = r[t];
+#pragma unroll
+        for (int t = 0; t < 6; t++) X[t] = __builtin_amdgcn_alignbyte(W[t + 1], W[t], sh);
+    }
+#endif
+    uint32_t Yw[6];
     if (kWin) {   // candidate bytes from the LDS window (chunks <= k+1 are in it by now)
         const bool tryT = k < B.nch && cT < p && cT >= 4u;
-        ring32(S, tryT ? cT - 4u : 0u, Yw);
+        const uint4 a = ring16(S, tryT ? cT - 4u : 0u);
+        const uint2 b = ring8(S, tryT ? cT + 12u : 16u);
+        Yw[0] = a.x; Yw[1] = a.y; Yw[2] = a.z; Yw[3] = a.w; Yw[4] = b.x; Yw[5] = b.y;
     }
-    const uint32_t (&Yr)[8] = kWin ? Yw : Y;
+    const uint32_t (&Yr)[6] = kWin ? Yw : Y;
 #define Y Yr
     const bool live = k < B.nch;
     R.hashable = live && p + 5u <= B.un;
     const bool can = live && p >= 1u && p <= B.mstart && B.n >= kMinLength;
     const uint32_t cL = 64u * (uint32_t)k + jL;
     // L candidate bytes in[cL-4, cL+12) from lane jL's own bytes
-    uint32_t Z[8];
+    uint32_t Z[4];
 #pragma unroll
-    for (int t = 0; t < 4; t++) Z[t] = (uint32_t)__shfl((int)X[t], (int)(jL & 63u), 64);
-#pragma unroll
-    for (int t = 4; t < 8; t++) Z[t] = 0u;
+    for (int t = 0; t < 4; t++) Z[t] = bperm(X[t], jL);
     const bool okT = can && cT < p && cT >= 4u && Y[1] == X[1];
     const bool okL = can && jL < (uint32_t)lane && cL != cT && Z[1] == X[1];   // jL = ~0 if noL
     R.lim = can ? B.mlimit - p : 0u;
     // measured unconditionally (selects, no branches): every lane reads Y, so the
-    // compiler sees the candidate load consumed on every path.  T to 28 bytes, L to 12:
+    // compiler sees the candidate load consumed on every path.  T to 20 bytes, L to 12:
     // L (the closer one) is taken when T is shorter than 12 and L at least as long,
     // and C2 continues the taken candidate from where C1 stopped
     // (tools/enc_model.c model4, pol 7 vs 0: ratio -0.1 %; measured -0.06 %, -3.4 % VALU).
@@ -421,37 +517,61 @@ __device__ __forceinline__ void prod_measure(const EncLds &S, const Blk &B, int 
     R.has = okT || okL;
     R.h = h;
 #undef Y
+}
+
+// S2(k), at the start of the second half (off C1's latency chain, next to C2(k-1)):
+// rank the truncated lanes and issue the stage-2 loads of the first kGroups of them
+template <bool SMALL, bool FAST = false>
+__device__ __forceinline__ void prod_stage2_issue(const EncLds &S, const Blk &B, int k, int lane,
+                                                  Part &R, uint32_t (&E)[4]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+    const uint64_t tb = wave_ballot(R.trunc1);
+    R.ntr = (uint32_t)__popcll(tb);
+    R.rank = lane_rank(tb);
+    uint32_t cb;
+    const bool ga = stage2_group(R, lane, 0u, p, cb, R.eo);
     if (kWin) {
-        ring32(S, R.trunc1 ? R.c + R.base : 0u, E);
+        const uint4 e = ring16(S, ga ? cb : 0u);
+        E[0] = e.x; E[1] = e.y; E[2] = e.z; E[3] = e.w;
         return;
     }
-    load32<SMALL>(B.in, B.n, R.trunc1 ? (int)(R.c + R.base) : 0, E,
-                  FAST || 64 * k + 123 <= B.n);
+    // cb + 16 <= c + base + kExt2 < p + 84 (c < p)
+    loadv<4>(B.in, B.un, ga ? cb : 0u, E, FAST || (!SMALL && 64 * k + 148 <= B.n));
 }
 
 // C2(k): finish the truncated lengths against the ring, hash match_end - 2 -> info
+template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int lane,
-                                            const Part &R, const uint32_t (&E)[8]) {
+                                            const Part &R, const uint32_t (&E)[4]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     uint32_t len = R.len;
     bool trunc = false;
-#ifdef APE_EXP_C2ANY
-    if (wave_any(R.trunc1)) {   // no lane reached C1's cap: nothing to finish
-#else
-    {   // unconditional for the same reason as in C1
-#endif
-        uint32_t O[8];
-        ring32(S, p + R.base, O);                // own bytes p+base .. p+base+32
-        const uint32_t ext = umin(first_diff_bit<0, 8>(O, E) >> 3, 32u);
+    {   // unconditional: a chunk without a truncated lane is rare (~1 in 250)
+        uint32_t mine = bperm(stage2_len(S, lane, R.eo, E), 4u * R.rank);
+        for (uint32_t first = kGroups; first < R.ntr; first += kGroups) {   // rare
+            uint32_t cb, eo, E2[4];
+            const bool ga = stage2_group(R, lane, first, p, cb, eo);
+            if (kWin) {
+                const uint4 e = ring16(S, ga ? cb : 0u);
+                E2[0] = e.x; E2[1] = e.y; E2[2] = e.z; E2[3] = e.w;
+            } else {
+                loadv<4>(B.in, B.un, ga ? cb : 0u, E2, FAST || (!SMALL && 64 * k + 148 <= B.n));
+            }
+            const uint32_t m2 = bperm(stage2_len(S, lane, eo, E2), 4u * (R.rank - first));
+            if (R.rank - first < kGroups) mine = m2;
+        }
         if (R.trunc1) {
-            len = umin(R.base + ext, R.lim);
-            trunc = ext == 32u && R.lim > R.base + 32u;
+            len = umin(R.base + mine, R.lim);
+            trunc = mine == kExt2 && R.lim > R.base + kExt2;
         }
     }
     uint32_t e2 = 0;
     if (R.has && !trunc) {
         const uint32_t at = p + len - 2u;         // match end - 2 (:680)
-        if (at + 5u <= B.un) e2 = I_E2 | (hash5(ring4(S, at), ring4(S, at + 4u)) << 16);
+        if (at + 5u <= B.un) {
+            const uint2 v = ring8(S, at);
+            e2 = I_E2 | (hash5(v.x, v.y) << 16);
+        }
     }
     S.info[k % 3][lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
                                          (R.has ? I_HAS : 0u) | (R.hashable ? I_HASHABLE : 0u) | e2,
@@ -804,19 +924,20 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             // Every stage runs on every step, past the last chunk too (it then loads
             // from the block start and records nothing), so the number of loads per
             // step -- and with it the waits -- is the same on every path.
-            // In flight, oldest first: A(s+2), Y(s+1) x2, E(s) x2 -> A(s+2) at 4.
-            vm_wait<kWin ? 0 : 4>();
+            // In flight, oldest first: A(s+2), Y(s+1) x2, E(s) -> A(s+2) at 3.
+            vm_wait<kWin ? 0 : 3>();
             prod_load<SMALL, F>(B, s + 3, lane, nxt.X);
             prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
-            // Y(s+1) x2, E(s) x2, A(s+3), Y(s+2) x2 -> Y(s+1) at 5
-            vm_wait<kWin ? 1 : 5>();
-            prod_measure<SMALL, F>(S, B, s + 1, lane, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q, nxt.E);
+            // Y(s+1) x2, E(s), A(s+3), Y(s+2) x2 -> Y(s+1) at 4
+            vm_wait<kWin ? 1 : 4>();
+            prod_measure<SMALL, F>(S, B, s + 1, lane, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q);
             STAT(5);
             __syncthreads();
             STAT(6);
-            // E(s) x2, A(s+3), Y(s+2) x2, E(s+1) x2 -> E(s) at 5
-            vm_wait<kWin ? 1 : 5>();
-            prod_finish(S, B, s, lane, cur.q, cur.E);
+            prod_stage2_issue<SMALL, F>(S, B, s + 1, lane, nxt.q, nxt.E);
+            // E(s), A(s+3), Y(s+2) x2, E(s+1) -> E(s) at 4
+            vm_wait<kWin ? 1 : 4>();
+            prod_finish<SMALL, F>(S, B, s, lane, cur.q, cur.E);
             STAT(7);
             __syncthreads();
             STAT(8);
@@ -828,14 +949,15 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             prod_lookup<SMALL>(S, B, k0, lane, P0.X, P0.cT, P0.jL, P0.h, P0.Y);
             prod_load<SMALL>(B, k0 + 2, lane, P0.X);
             prod_lookup<SMALL>(S, B, k0 + 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
-            prod_measure<SMALL>(S, B, k0, lane, P0.Y, P0.cT, P0.jL, P0.h, P0.q, P0.E);
+            prod_measure<SMALL>(S, B, k0, lane, P0.Y, P0.cT, P0.jL, P0.h, P0.q);
+            prod_stage2_issue<SMALL>(S, B, k0, lane, P0.q, P0.E);
         }
         // nothing in flight at the loop entry, so the loop's counter waits depend only
         // on its own issue order (once per block)
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
         // Steps whose three loads all lie inside the block (A(s+3): 64(s+3)+72 <= n,
-        // Y(s+2): 64(s+2)+91, E(s+1): 64(s+1)+123) run a loop without the edge paths;
+        // Y(s+2): 64(s+2)+83, E(s+1): 64(s+1)+148) run a loop without the edge paths;
         // the last few steps run the general one.
         const int nfast_abs = SMALL ? 0 : (int)umin((uint32_t)(B.n >= 264 ? (B.n - 264) / 64 + 1 : 0),
                                                     (uint32_t)nsteps);

@@ -27,7 +27,7 @@ def main():
         amd.compress_batch(src, sizes, comp, csz)
         amd.decompress_batch(comp, csz, out, dres, dst_caps=sizes)
     torch.cuda.synchronize()
-    print("ok", bool((dres == n).all()), "ratio %.4f" % (nb * n / int(csz.sum())))
+    print("ok", bool((dres == n).all()), "ratio %.4f" % (nb * n / max(1, int(csz.sum()))))
 
 
 if __name__ == "__main__":
