@@ -247,6 +247,14 @@ __device__ __forceinline__ uint32_t div255(uint32_t e) {
     return (uint32_t)__umul24(e, 0x8081u) >> 23;
 }
 
+// 255 x (low 24 bits of v), one full-rate v_mul_u32_u24 (written out: the compiler
+// turns __umul24(v, 255) into a mask and a quarter-rate v_mul_lo_u32)
+__device__ __forceinline__ uint32_t mul255(uint32_t v) {
+    uint32_t r;
+    asm("v_mul_u32_u24 %0, 0xff, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+
 // bytes after a 15 nibble: v < 15 -> 0, else (v - 15) / 255 + 1 -- both are
 // (v + 240) / 255 (v + 240 < 255 below 15; one full-rate multiply, no select)
 __device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {
@@ -496,8 +504,9 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     uint32_t Z[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) Z[t] = bperm(X[t], jL);
-    const bool okT = can && cT < p && cT >= 4u && Y[1] == X[1];
-    const bool okL = can && jL < (uint32_t)lane && cL != cT && Z[1] == X[1];   // jL = ~0 if noL
+    // (bitwise on bools: lane masks combined by the scalar unit, no materialised 0/1)
+    const bool okT = can & (cT < p) & (cT >= 4u) & (Y[1] == X[1]);
+    const bool okL = can & (jL < (uint32_t)lane) & (cL != cT) & (Z[1] == X[1]);   // jL = ~0 if noL
     R.lim = can ? B.mlimit - p : 0u;
     // measured unconditionally (selects, no branches): every lane reads Y, so the
     // compiler sees the candidate load consumed on every path.  T to 20 bytes, L to 12:
@@ -507,14 +516,14 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     const uint32_t eT = eager(X, Y);
     const uint32_t eL = umin((first_diff_bit<2, 4>(X, Z) >> 3) + 4u, kEagerL);
     const uint32_t lT = okT ? eT : 0u, lL = okL ? eL : 0u;
-    const bool pickL = okL && (!okT || (lT < kEagerL && lL >= lT));
+    const bool pickL = okL & (!okT | ((lT < kEagerL) & (lL >= lT)));
     R.c = pickL ? cL : cT;
     R.len = pickL ? lL : lT;
     R.base = pickL ? kEagerL : kEagerLen;
-    R.trunc1 = R.len >= R.base && R.lim > R.base;
-    if (R.len > R.lim) R.len = R.lim;
+    R.trunc1 = (R.len >= R.base) & (R.lim > R.base);
+    R.len = umin(R.len, R.lim);
     R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
-    R.has = okT || okL;
+    R.has = okT | okL;
     R.h = h;
 #undef Y
 }
@@ -705,7 +714,7 @@ __device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk 
     if (O.q0 >= P + 64u) return;              // covered by a match from earlier chunks
     // catch-up limits: a member's backward extension stops at the previous end
     const uint32_t anchor0 = W.anchor;
-    const bool mem = (O.members >> lane) & 1ull;
+    const bool mem = lane_in(O.members);
     const uint32_t p = P + (uint32_t)lane;
     const uint32_t end = mem ? p + O.Lf : 0u;
     const uint32_t imax = wave_incl_max(end);
@@ -726,8 +735,8 @@ __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int
                                              const WalkOut &O) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const uint2 iv = O.iv;
-    if (((O.walked >> lane) & 1ull) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
-    const bool mem = (O.members >> lane) & 1ull;
+    if (lane_in(O.walked) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
+    const bool mem = lane_in(O.members);
     const uint32_t fwd = O.m_len - O.m_back;      // match length from p
     // match_end - 2 (:680): hashed by the producer unless the walker extended the match
     uint32_t e2h = (iv.x >> 16) & (kHSize - 1);
@@ -783,7 +792,7 @@ __device__ __forceinline__ void emit_prepare(const EncLds &S, const Blk &B, int 
     if (!C.members) return;
     const uint2 wr = S.wres[k & 1][lane];
     const uint32_t off = S.info[k % 3][lane].y & 0xFFFFu;
-    const bool mem = (C.members >> lane) & 1ull;
+    const bool mem = lane_in(C.members);
     const uint32_t m_len = wr.x & 0xFFFFFu, m_back = wr.x >> 20;
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const uint32_t ms = p - m_back;            // match start after catch-up
@@ -813,7 +822,7 @@ __device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int kA, int 
     // runs in the first half of step kA + 4, while the producer copies chunk kA + 6
     // into the ring (or after the last step): input [rlo, P + 384) is intact there
     const uint32_t rlo = P + 448u > kRingE ? P + 448u - kRingE : 0u;
-    const bool memA = (E.A.members >> lane) & 1ull, memB = (E.Bc.members >> lane) & 1ull;
+    const bool memA = lane_in(E.A.members), memB = lane_in(E.Bc.members);
     const uint32_t exA = E.A.ex, exB = totA + E.Bc.ex;
     // member starts, ~0 for other lanes: the window tests below are single compares
     const uint32_t sA = memA ? exA : 0xFFFFFFFFu, sB = memB ? exB : 0xFFFFFFFFu;
@@ -857,8 +866,8 @@ __device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int kA, int 
         if (rr >= lit_at && rr < off_at && a < rlo) v = B.in[a];   // older than the ring (rare)
         // length extension bytes: 255 while more than 254 remain, then the rest
         // (the i-th byte after the nibble is min(255, v - 15 - 255 i))
-        const uint32_t vl = umin(rl - 15u - (uint32_t)__umul24(rr - 1u, 255u), 255u);
-        const uint32_t vm = umin(rml - 15u - (uint32_t)__umul24(rr - off_at - 2u, 255u), 255u);
+        const uint32_t vl = umin(rl - 15u - mul255(rr - 1u), 255u);
+        const uint32_t vm = umin(rml - 15u - mul255(rr - off_at - 2u), 255u);
         const uint32_t vo = rr == off_at ? (roff & 0xFFu) : (roff >> 8);
         v = rr < off_at ? v : (rr < off_at + 2u ? vo : vm);
         v = rr < lit_at ? vl : v;

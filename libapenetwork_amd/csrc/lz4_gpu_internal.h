@@ -50,6 +50,9 @@ __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 // costs a v_cndmask + v_cmp per vote where the condition already is a lane mask.
 __device__ __forceinline__ uint64_t wave_ballot(bool c) { return __builtin_amdgcn_ballot_w64(c); }
 __device__ __forceinline__ bool wave_any(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
+// This lane's bit of a wave-uniform mask as a lane predicate: the mask itself becomes the
+// condition register (no shift / and / 64-bit compare per lane).
+__device__ __forceinline__ bool lane_in(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 
 // DPP lane moves (GFX9-family controls, available on gfx950): lanes whose
 // source is outside the row / masked off keep `old`.
