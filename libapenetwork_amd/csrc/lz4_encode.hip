@@ -89,10 +89,11 @@ constexpr uint32_t kScr = 1u << APE_LZ4_SCRBITS;  // in-chunk candidate scratch 
 constexpr int kSmall = 128;          // smaller blocks take the byte-load path
 
 
-// info.x: len (8) | back << 8 (3) | trunc << 11 | has << 12 | hashable << 13 |
-//         e2 << 14 | hash(match_end - 2) << 16;   info.y: offset | h << 16
-constexpr uint32_t I_TRUNC = 1u << 11, I_HAS = 1u << 12, I_HASHABLE = 1u << 13,
-                   I_E2 = 1u << 14;
+// info.x: len (7) | trunc << 7 | back << 8 (3) | hashable << 13;   info.y: offset | h << 16
+// The low byte is the walker's hop as it is: 0 = no candidate (a found match has len >= 4),
+// len, or len | 0x80 = unfinished (len <= kEagerLen + kExt2 < 128).
+constexpr uint32_t I_TRUNC = 1u << 7, I_HASHABLE = 1u << 13;
+static_assert(kEagerLen + kExt2 < 128u, "len fits 7 bits");
 
 struct __attribute__((aligned(16))) EncLds {
     uint16_t tab[kHSize];
@@ -405,7 +406,7 @@ __device__ __forceinline__ void prod_fetch_t(const Blk &B, int k, int lane, uint
     loadv<6>(B.in, B.un, tryT ? cT - 4u : 0u, Y, FAST || (!SMALL && 64 * k + 83 <= B.n));
 }
 
-// B(k): hash, table + in-chunk candidates, T fetch issue, ring copy
+// B(k): hash, table + in-chunk candidates, T fetch issue
 template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int lane,
                                             const uint32_t (&X)[2], uint32_t &cT, uint32_t &jL,
@@ -424,14 +425,39 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
         wave_sync();
         if (hashable) S.scr[hs] = 0xFFFFFFFFu;
     }
-    // ring copy of this chunk (own bytes for C1, stage 2, match_end - 2, literals);
-    // zero past the block end
-    if (live) {
+    if (!kWin) prod_fetch_t<SMALL, FAST>(B, k, lane, cT, Y);
+}
+
+// R(k): ring copy of chunk k (own bytes for C1 and stage 2, match_end - 2, literals; zero
+// past the block end), in the second half of step k - 3, so that C1(k - 1)'s ring read can
+// start a step later without waiting for anything
+__device__ __forceinline__ void prod_ring(EncLds &S, const Blk &B, int k, int lane,
+                                          const uint32_t (&X)[2]) {
+    if (k < B.nch) {
+        const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
         const uint8_t by = (uint8_t)X[0];
         ((uint8_t *)S.ring)[p & (kRingE - 1)] = by;
         if (((64u * (uint32_t)k) & (kRingE - 1)) == 0u) ((uint8_t *)S.ring)[kRingE + lane] = by;
     }
-    if (!kWin) prod_fetch_t<SMALL, FAST>(B, k, lane, cT, Y);
+}
+
+// own bytes in[p-4, p+20) of chunk k from the ring (ring tail = 0 before 0)
+__device__ __forceinline__ void prod_own(const EncLds &S, int k, int lane, uint32_t (&X)[6]) {
+    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
+#ifdef APE_EXP_UNALIGNED_RING
+    const uint4 a = ring16(S, p - 4u);
+    const uint2 b = ring8(S, p + 12u);
+    X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w; X[4] = b.x; X[5] = b.y;
+#else
+    // 7 aligned dwords, 6 alignbytes
+    const uint32_t *r = S.ring + (((p - 4u) >> 2) & (kRingE / 4 - 1));
+    const uint32_t sh = p & 3u;
+    uint32_t W[7];
+#pragma unroll
+    for (int t = 0; t < 7; t++) W[t] = r[t];
+#pragma unroll
+    for (int t = 0; t < 6; t++) X[t] = __builtin_amdgcn_alignbyte(W[t + 1], W[t], sh);
+#endif
 }
 
 // Stage-2 group of this lane for the truncated lanes of ranks [first, first + kGroups):
@@ -466,27 +492,9 @@ __device__ __forceinline__ uint32_t stage2_len(const EncLds &S, int lane, uint32
 // the stage-2 loads of the first kGroups of them
 template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int lane,
-                                             const uint32_t (&Y)[6], uint32_t cT, uint32_t jL,
-                                             uint32_t h, Part &R) {
+                                             const uint32_t (&X)[6], const uint32_t (&Y)[6],
+                                             uint32_t cT, uint32_t jL, uint32_t h, Part &R) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-    uint32_t X[6];                   // own bytes in[p-4, p+20) (ring tail = 0 before 0)
-#ifdef APE_EXP_UNALIGNED_RING
-    {
-        const uint4 a = ring16(S, p - 4u);
-        const uint2 b = ring8(S, p + 12u);
-        X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w; X[4] = b.x; X[5] = b.y;
-    }
-#else
-    {   // 7 aligned dwords, 6 alignbytes
-        const uint32_t *r = S.ring + (((p - 4u) >> 2) & (kRingE / 4 - 1));
-        const uint32_t sh = p & 3u;
-        uint32_t W[7];
-#pragma unroll
-        for (int t = 0; t < 7; t++) W[t] = r[t];
-#pragma unroll
-        for (int t = 0; t < 6; t++) X[t] = __builtin_amdgcn_alignbyte(W[t + 1], W[t], sh);
-    }
-#endif
     uint32_t Yw[6];
     if (kWin) {   // candidate bytes from the LDS window (chunks <= k+1 are in it by now)
         const bool tryT = k < B.nch && cT < p && cT >= 4u;
@@ -548,7 +556,7 @@ __device__ __forceinline__ void prod_stage2_issue(const EncLds &S, const Blk &B,
     loadv<4>(B.in, B.un, ga ? cb : 0u, E, FAST || (!SMALL && 64 * k + 148 <= B.n));
 }
 
-// C2(k): finish the truncated lengths against the ring, hash match_end - 2 -> info
+// C2(k): finish the truncated lengths against the ring -> info
 template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int lane,
                                             const Part &R, const uint32_t (&E)[4]) {
@@ -574,16 +582,8 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
             trunc = mine == kExt2 && R.lim > R.base + kExt2;
         }
     }
-    uint32_t e2 = 0;
-    if (R.has && !trunc) {
-        const uint32_t at = p + len - 2u;         // match end - 2 (:680)
-        if (at + 5u <= B.un) {
-            const uint2 v = ring8(S, at);
-            e2 = I_E2 | (hash5(v.x, v.y) << 16);
-        }
-    }
     S.info[k % 3][lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
-                                         (R.has ? I_HAS : 0u) | (R.hashable ? I_HASHABLE : 0u) | e2,
+                                         (R.hashable ? I_HASHABLE : 0u),
                                      (R.has ? p - R.c : 0u) | (R.h << 16));
 }
 
@@ -659,12 +659,11 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     O.m_back = O.m_len = O.an = 0;
     O.iv = S.info[k % 3][lane];
     O.q0 = W.q;
-    O.Lf = O.iv.x & 0xFFu;                               // forward match length
+    O.Lf = O.iv.x & 0x7Fu;                               // forward match length
     if (W.q >= P + 64u) return;               // a match from earlier chunks covers it
     const uint2 iv = O.iv;
-    const bool has = (iv.x & I_HAS) != 0u, trunc = (iv.x & I_TRUNC) != 0u;
-    const uint64_t Hm = wave_ballot(has);
-    const uint32_t Lh = has ? (trunc ? 0x80u : O.Lf) : 0u;   // hop; 0x80 = unfinished
+    const uint64_t Hm = wave_ballot(O.Lf != 0u);          // lanes with a match
+    const uint32_t Lh = iv.x & 0xFFu;                     // hop; | 0x80 = unfinished
     uint32_t rel = W.q - P;
     uint64_t M = 0;
     for (;;) {
@@ -695,7 +694,7 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
         if (h & 0x80u) {
             const uint32_t me = P + j;
             const uint32_t cm = me - (lane_val(iv.y, (int)j) & 0xFFFFu);
-            const uint32_t Le = extend_match(B, me, cm, lane_val(iv.x, (int)j) & 0xFFu, lane);
+            const uint32_t Le = extend_match(B, me, cm, h & 0x7Fu, lane);
             if ((uint32_t)lane == j) O.Lf = Le;
             rel = j + Le;
         } else {
@@ -738,25 +737,29 @@ __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int
     if (lane_in(O.walked) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
     const bool mem = lane_in(O.members);
     const uint32_t fwd = O.m_len - O.m_back;      // match length from p
-    // match_end - 2 (:680): hashed by the producer unless the walker extended the match
-    uint32_t e2h = (iv.x >> 16) & (kHSize - 1);
-    bool e2ok = mem && (iv.x & I_E2) && !(iv.x & I_TRUNC);
-    if (mem && (iv.x & I_TRUNC)) {
-        const uint32_t e2 = p + fwd - 2u;
-        if (e2 + 5u <= B.un) {
+    // match_end - 2 (:680) of the members, hashed here (off the producer's chain): from the
+    // ring -- it holds chunks k - 12 .. k + 3 now, and a match the producer finished ends
+    // before p + 85 -- or, for a match the walker extended, from the input
+    const uint32_t e2 = p + fwd - 2u;
+    const bool e2ok = mem && e2 + 5u <= B.un;
+    uint32_t e2h = 0;
+    if (e2ok) {
+        if (!(iv.x & I_TRUNC)) {
+            const uint2 v = ring8(S, e2);
+            e2h = hash5(v.x, v.y);
+        } else {
             uint32_t lo32 = 0, b4 = 0;
             for (uint32_t t = 0; t < 5u; t++) {
                 const uint32_t by = B.in[e2 + t];
                 if (t < 4) lo32 |= by << (8 * t); else b4 = by;
             }
             e2h = hash5(lo32, b4);
-            e2ok = true;
         }
     }
     // one wave's LDS operations complete in order: the walked-position inserts above
     // land before these (compiler barrier only)
     __builtin_amdgcn_sched_barrier(0);
-    if (e2ok) S.tab[e2h] = (uint16_t)(p + fwd - 2u);
+    if (e2ok) S.tab[e2h] = (uint16_t)e2;
     S.wres[k & 1][lane] = make_uint2(O.m_len | (O.m_back << 20), O.an);
     if (lane == 0) {
         S.wmem[k & 1][0] = (uint32_t)O.members;
@@ -935,17 +938,20 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             // step -- and with it the waits -- is the same on every path.
             // In flight, oldest first: A(s+2), Y(s+1) x2, E(s) -> A(s+2) at 3.
             vm_wait<kWin ? 0 : 3>();
+            uint32_t X6[6];   // C1(s+1)'s own bytes: in the ring since last step, read first
+            prod_own(S, s + 1, lane, X6);
             prod_load<SMALL, F>(B, s + 3, lane, nxt.X);
             prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
             // Y(s+1) x2, E(s), A(s+3), Y(s+2) x2 -> Y(s+1) at 4
             vm_wait<kWin ? 1 : 4>();
-            prod_measure<SMALL, F>(S, B, s + 1, lane, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q);
+            prod_measure<SMALL, F>(S, B, s + 1, lane, X6, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q);
             STAT(5);
             __syncthreads();
             STAT(6);
             prod_stage2_issue<SMALL, F>(S, B, s + 1, lane, nxt.q, nxt.E);
-            // E(s), A(s+3), Y(s+2) x2, E(s+1) -> E(s) at 4
-            vm_wait<kWin ? 1 : 4>();
+            // E(s), A(s+3), Y(s+2) x2, E(s+1) -> E(s) and A(s+3) at 3
+            vm_wait<kWin ? 0 : 3>();
+            prod_ring(S, B, s + 3, lane, nxt.X);
             prod_finish<SMALL, F>(S, B, s, lane, cur.q, cur.E);
             STAT(7);
             __syncthreads();
@@ -955,10 +961,15 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         if (nch > k0) {  // prologue: A(k0), A(k0+1), B(k0), A(k0+2), B(k0+1), C1(k0)
             prod_load<SMALL>(B, k0, lane, P0.X);
             prod_load<SMALL>(B, k0 + 1, lane, P1.X);
+            prod_ring(S, B, k0, lane, P0.X);
             prod_lookup<SMALL>(S, B, k0, lane, P0.X, P0.cT, P0.jL, P0.h, P0.Y);
             prod_load<SMALL>(B, k0 + 2, lane, P0.X);
+            prod_ring(S, B, k0 + 1, lane, P1.X);
             prod_lookup<SMALL>(S, B, k0 + 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
-            prod_measure<SMALL>(S, B, k0, lane, P0.Y, P0.cT, P0.jL, P0.h, P0.q);
+            prod_ring(S, B, k0 + 2, lane, P0.X);
+            uint32_t X6[6];
+            prod_own(S, k0, lane, X6);
+            prod_measure<SMALL>(S, B, k0, lane, X6, P0.Y, P0.cT, P0.jL, P0.h, P0.q);
             prod_stage2_issue<SMALL>(S, B, k0, lane, P0.q, P0.E);
         }
         // nothing in flight at the loop entry, so the loop's counter waits depend only
