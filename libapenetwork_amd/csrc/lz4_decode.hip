@@ -59,7 +59,7 @@ static_assert(kKeep >= 64 && kKeep % 16 == 0 && kWinB >= kKeep + 1024 && kWinB %
 constexpr int kStage = APE_LZ4_DSTAGE;   // staged compressed bytes (a multiple of 256)
 constexpr int kWinNeed = 84;     // a parse window reads up to P + 63 + 21
 constexpr int kBatch = 64;       // descriptors per copy batch (one per lane)
-constexpr int kMaxDesc = kBatch + 48;   // held before a copy: < 64, + <= 44 per parse step, + 1
+constexpr int kMaxDesc = kBatch + 44;   // held before a copy: <= 63, + <= 44 per parse step, + 1
 constexpr uint32_t kLaneMax = 64;  // longest match one lane copies (4 x 16 bytes)
 
 struct __attribute__((aligned(16))) WaveLds {
