@@ -11,7 +11,7 @@
 //
 // One 192-thread workgroup (three waves, one role each) per block; a batch holds
 // ~1M blocks, so most of the parallelism comes from many blocks in flight (8 per
-// CU).  Per block the LDS (20.0 KiB) holds the reference's own hash table (8192 x
+// CU).  Per block the LDS (19.9 KiB) holds the reference's own hash table (8192 x
 // u16, 13-bit hash of 5 bytes, :449-462), a 1 KiB ring of recent input and the
 // hand-over records between the roles.  The input stays in HBM/L2.
 //
@@ -23,15 +23,18 @@
 //     B(s+2)  hash in[p, p+5), read candidate T = table[h] (positions walked
 //             earlier plus match_end - 2, inserted as the reference does:
 //             :595-619, :680-706) and L = the earliest lane of the chunk with the
-//             same hash bits; copy the chunk into the ring; load in[T-4, T+28);
-//     C1(s+1) verify 4 bytes for T and L, measure both to 28 bytes forward and 4
-//             backward, keep the longer (then closer); load 32 more for a 28;
-//     C2(s)   (second half) finish those to 60 bytes, hash match_end - 2 ->
-//             match info of chunk s in LDS.
+//             same hash bits; load in[T-4, T+16);
+//     C1(s+1) own bytes from the ring, verify 4 bytes for T and L, measure T to 16
+//             bytes and L to 12 forward and both 4 backward, keep the longer;
+//     S2(s+1) (second half) the truncated candidates, ranked and pushed into groups
+//             of 4 lanes, each group loading the 64 bytes that follow;
+//     R(s+3)  copy chunk s+3 into the ring;
+//     C2(s)   finish the truncated lengths (+64 bytes) -> match info of chunk s.
 //   WALKER (wave 0), chunk s-1: the greedy chain on the scalar unit (hops over the
 //     match lanes of a ballot mask), catch-up into pending literals (:623-627),
-//     the wave-wide extension of matches >= 60 bytes; second half: table inserts
-//     of the walked positions and match_end - 2 (:680), never overlapping B.
+//     the wave-wide extension of matches >= 80 bytes; second half: table inserts
+//     of the walked positions and match_end - 2 (:680, hashed here from the ring),
+//     never overlapping B.
 //   EMITTER (wave 2), chunk s-2: sizes and prefix-sum offsets of the sequences,
 //     then each lane of a 64-byte output window computes its output byte; the
 //     last literals (:732-751) are copied with 16-byte moves.
@@ -67,9 +70,14 @@ namespace {
 #endif
 constexpr int kHLog = APE_LZ4_HLOG;
 constexpr int kHSize = 1 << kHLog;
-constexpr uint32_t kEagerLen = 20;   // match bytes measured by C1 (T candidate)
+#ifndef APE_LZ4_EAGER_T
+#define APE_LZ4_EAGER_T 16
+#endif
+constexpr uint32_t kEagerLen = APE_LZ4_EAGER_T;   // match bytes measured by C1 (T candidate)
+static_assert(kEagerLen == 16 || kEagerLen == 20, "C1 measures T to 16 or 20 bytes");
+constexpr int kYW = (int)(kEagerLen + 4u) / 4;   // T-candidate dwords loaded: in[T-4, T+kEagerLen)
 constexpr uint32_t kEagerL = 12;     // ... for the in-chunk candidate L
-// Stage 2 (C2) measures only the candidates C1 left truncated (~8 % of the lanes on App.
+// Stage 2 (C2) measures only the candidates C1 left truncated (~13 % of the lanes on App.
 // C data), compacted into groups of 4 lanes that compare 16 bytes each: 64 more bytes
 // per candidate, 16 candidates per pass (a second pass is rare).
 constexpr uint32_t kExt2 = 64;
@@ -234,7 +242,7 @@ __device__ __forceinline__ uint32_t first_diff_bit(const uint32_t (&A)[NA], cons
 
 // common length of X and Y from byte 4 (dword 1) on, up to kEagerLen
 __device__ __forceinline__ uint32_t eager(const uint32_t (&X)[6], const uint32_t (&Y)[6]) {
-    return umin((first_diff_bit<2, 6>(X, Y) >> 3) + 4u, kEagerLen);
+    return umin((first_diff_bit<2, kYW>(X, Y) >> 3) + 4u, kEagerLen);
 }
 
 // bytes equal just before the match (in[p-1] == in[c-1], ...), 0..4
@@ -306,16 +314,18 @@ __device__ __forceinline__ uint2 ring8(const EncLds &S, uint32_t x) {
 // NW dwords in[pos, pos + 4 NW) (NW = 4 or 6).  fast: the window lies inside [0, n)
 // (vector loads); otherwise byte loads, bytes outside [0, n) read as 0 (the edge steps
 // and blocks below kSmall only).
-template <int NW>
-__device__ __forceinline__ void loadv(gcu8 *in, uint32_t un, uint32_t pos, uint32_t (&X)[NW],
+template <int NW, int NA>
+__device__ __forceinline__ void loadv(gcu8 *in, uint32_t un, uint32_t pos, uint32_t (&X)[NA],
                                       bool fast) {
-    static_assert(NW == 4 || NW == 6, "loadv");
+    static_assert(NW >= 4 && NW <= 6 && NW <= NA, "loadv");
     if (fast) {
         const uint4 a = gload16(in + pos);
         X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w;
-        if (NW == 6) {
+        if constexpr (NW == 6) {
             const uint2 b = gload8(in + pos + 16u);
             X[4] = b.x; X[5] = b.y;
+        } else if constexpr (NW == 5) {
+            X[4] = gload4(in + pos + 16u);
         }
         return;
     }
@@ -373,7 +383,7 @@ struct Part {                        // C1 result of one chunk, finished by C2
 // C1 for C2.
 struct PSet {
     uint32_t X[2];                   // own bytes in[p, p+8) of the chunk B works on next
-    uint32_t Y[6];                   // T-candidate bytes in[T-4, T+20)
+    uint32_t Y[6];                   // T-candidate bytes in[T-4, T+kEagerLen)
     uint32_t E[4];                   // stage-2 candidate bytes of this lane's group
     uint32_t cT, jL, h;
     Part q;
@@ -395,7 +405,7 @@ __device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_
         if (pos + t < B.un) X[t >> 2] |= (uint32_t)B.in[pos + t] << (8 * (t & 3));
 }
 
-// T candidate bytes in[T-4, T+20) of chunk k (issued one step before C1 consumes them).
+// T candidate bytes in[T-4, T+kEagerLen) of chunk k (issued one step before C1 consumes them).
 // Candidates below position 4 are skipped: their 4 bytes of backward context would start
 // before the block (never-written slots read as 0).
 template <bool SMALL, bool FAST = false>
@@ -403,7 +413,7 @@ __device__ __forceinline__ void prod_fetch_t(const Blk &B, int k, int lane, uint
                                              uint32_t (&Y)[6]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const bool tryT = k < B.nch && cT < p && cT >= 4u;
-    loadv<6>(B.in, B.un, tryT ? cT - 4u : 0u, Y, FAST || (!SMALL && 64 * k + 83 <= B.n));
+    loadv<kYW>(B.in, B.un, tryT ? cT - 4u : 0u, Y, FAST || (!SMALL && 64 * k + 83 <= B.n));
 }
 
 // B(k): hash, table + in-chunk candidates, T fetch issue
@@ -488,7 +498,7 @@ __device__ __forceinline__ uint32_t stage2_len(const EncLds &S, int lane, uint32
     return umin(d >> 3, kExt2);
 }
 
-// C1(k): verify / measure to 20 bytes / pick; queue the truncated candidates and issue
+// C1(k): verify / measure to kEagerLen bytes / pick; queue the truncated candidates and issue
 // the stage-2 loads of the first kGroups of them
 template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int lane,
@@ -517,7 +527,7 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     const bool okL = can & (jL < (uint32_t)lane) & (cL != cT) & (Z[1] == X[1]);   // jL = ~0 if noL
     R.lim = can ? B.mlimit - p : 0u;
     // measured unconditionally (selects, no branches): every lane reads Y, so the
-    // compiler sees the candidate load consumed on every path.  T to 20 bytes, L to 12:
+    // compiler sees the candidate load consumed on every path.  T to 16 bytes, L to 12:
     // L (the closer one) is taken when T is shorter than 12 and L at least as long,
     // and C2 continues the taken candidate from where C1 stopped
     // (tools/enc_model.c model4, pol 7 vs 0: ratio -0.1 %; measured -0.06 %, -3.4 % VALU).
@@ -552,7 +562,7 @@ __device__ __forceinline__ void prod_stage2_issue(const EncLds &S, const Blk &B,
         E[0] = e.x; E[1] = e.y; E[2] = e.z; E[3] = e.w;
         return;
     }
-    // cb + 16 <= c + base + kExt2 < p + 84 (c < p)
+    // cb + 16 <= c + base + kExt2 < p + 80 (c < p)
     loadv<4>(B.in, B.un, ga ? cb : 0u, E, FAST || (!SMALL && 64 * k + 148 <= B.n));
 }
 
@@ -739,7 +749,7 @@ __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int
     const uint32_t fwd = O.m_len - O.m_back;      // match length from p
     // match_end - 2 (:680) of the members, hashed here (off the producer's chain): from the
     // ring -- it holds chunks k - 12 .. k + 3 now, and a match the producer finished ends
-    // before p + 85 -- or, for a match the walker extended, from the input
+    // before p + 81 -- or, for a match the walker extended, from the input
     const uint32_t e2 = p + fwd - 2u;
     const bool e2ok = mem && e2 + 5u <= B.un;
     uint32_t e2h = 0;
