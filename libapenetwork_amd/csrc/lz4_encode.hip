@@ -948,19 +948,24 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             // step -- and with it the waits -- is the same on every path.
             // In flight, oldest first: A(s+2), Y(s+1) x2, E(s) -> A(s+2) at 3.
             vm_wait<kWin ? 0 : 3>();
+            STAT(9);   // (stats build: load waits)
             uint32_t X6[6];   // C1(s+1)'s own bytes: in the ring since last step, read first
             prod_own(S, s + 1, lane, X6);
             prod_load<SMALL, F>(B, s + 3, lane, nxt.X);
             prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
             // Y(s+1) x2, E(s), A(s+3), Y(s+2) x2 -> Y(s+1) at 4
+            STAT(5);
             vm_wait<kWin ? 1 : 4>();
+            STAT(9);
             prod_measure<SMALL, F>(S, B, s + 1, lane, X6, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q);
             STAT(5);
             __syncthreads();
             STAT(6);
             prod_stage2_issue<SMALL, F>(S, B, s + 1, lane, nxt.q, nxt.E);
             // E(s), A(s+3), Y(s+2) x2, E(s+1) -> E(s) and A(s+3) at 3
+            STAT(7);
             vm_wait<kWin ? 0 : 3>();
+            STAT(9);
             prod_ring(S, B, s + 3, lane, nxt.X);
             prod_finish<SMALL, F>(S, B, s, lane, cur.q, cur.E);
             STAT(7);
@@ -1061,7 +1066,9 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         }
 #else
         if (work && E.pend && E.kA == s - 4) {   // the pair prepared in steps s-2, s-1
+#ifndef APE_EXP_NOWRITE   // diagnostic: instruction count without the output windows
             emit_write(S, B, s - 4, lane, E);
+#endif
             E.pend = false;
         }
 #endif

@@ -15,9 +15,9 @@ sys.path.insert(0, ROOT)
 
 DEC = ["parse", "copy", "(batches)", "(passes after round 1)", "(restages)", "(coop matches)",
        "(window slides)", "", "", "", "(blocks)", "", "", "", "", ""]
-ENC = ["W walk", "W publish", "E load", "W wait end", "W wait mid", "P F+M+H+L",
-       "P wait mid", "P wait end", "(sequences)", "(batches)", "(steps x3 waves)",
-       "(walker extensions)", "E store",
+ENC = ["W walk", "W publish", "E write", "W wait end", "W wait mid", "P A+B+C1",
+       "P wait mid", "P C2 + S2 + R", "P wait end", "P load waits", "(steps x3 waves)",
+       "(members)", "E prepare",
        "(blocks)", "E wait mid", "E wait end"]
 
 
