@@ -816,7 +816,9 @@ __device__ __forceinline__ void emit_prepare(const EncLds &S, const Blk &B, int 
     C.ex = wave_excl_scan(size);
     C.tot = lane_val(C.ex + size, 63);
     C.mo = ml | (off << 16);
-    if ((uint64_t)E.o + before + C.tot > B.cap) {
+    // (32-bit: o <= cap < 2^31 and a chunk's output < 2^21, so the sum cannot wrap; a
+    // 64-bit compare of these uniform values went to the vector unit)
+    if (E.o + before + C.tot > B.cap) {
         E.overflow = true;
         C.members = 0;
         C.tot = 0;
