@@ -878,7 +878,15 @@ __device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int kA, int 
         const uint32_t lit_at = 1u + ext_bytes(rl), off_at = lit_at + rl;
         const uint32_t a = r_an + (rr - lit_at);         // literal source position
         uint32_t v = ((const uint8_t *)S.ring)[a & (kRingE - 1)];
-        if (rr >= lit_at && rr < off_at && a < rlo) v = B.in[a];   // older than the ring (rare)
+        // a literal older than the ring (rare) comes from the input.  The load sits in a
+        // wave-uniform branch with its own wait: as a plain conditional load, the compiler's
+        // wait before the merged value was an s_waitcnt vmcnt(0) on every window, which (vmcnt
+        // counts stores too) drained the previous windows' output stores each time.
+        const bool older = rr >= lit_at && rr < off_at && a < rlo;
+        if (wave_any(older)) {
+            if (older) v = B.in[a];
+            vm_wait<0>();
+        }
         // length extension bytes: 255 while more than 254 remain, then the rest
         // (the i-th byte after the nibble is min(255, v - 15 - 255 i))
         const uint32_t vl = umin(rl - 15u - mul255(rr - 1u), 255u);
