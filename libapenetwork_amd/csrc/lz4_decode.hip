@@ -123,22 +123,27 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // Aligned dword of the compressed block at byte offset `off` (src + off is
-// 4-aligned); bytes outside [0, csize) read as 0 and nothing beyond that dword
-// (which cannot cross a page) is touched.
-__device__ __forceinline__ uint32_t src_dword(gcu8 *src, int csize, int off) {
-    if (off >= csize || off <= -4) return 0u;
-    uint32_t v = *(__attribute__((address_space(1))) const uint32_t *)(src + off);
-    if (off < 0) v &= 0xFFFFFFFFu << (8 * (-off));
-    if (off + 4 > csize) v &= 0xFFFFFFFFu >> (8 * (off + 4 - csize));
-    return v;
+// 4-aligned); bytes outside [0, csize) read as 0 and nothing beyond a dword that
+// intersects [0, csize) is touched (a dword outside it loads the one at `first`, the
+// aligned dword holding byte 0).  Loaded unconditionally and masked with selects, so
+// a stage's loads are all in flight together (a branch around each load had made the
+// compiler wait for every one before issuing the next).
+__device__ __forceinline__ uint32_t src_dword(gcu8 *src, int csize, int off, int first) {
+    const bool in = off < csize && off > -4;
+    uint32_t v = *(__attribute__((address_space(1))) const uint32_t *)(src + (in ? off : first));
+    const uint32_t lo = off < 0 ? 0xFFFFFFFFu << (8 * (umin((uint32_t)-off, 3u))) : 0xFFFFFFFFu;
+    const uint32_t hi = off + 4 > csize ? 0xFFFFFFFFu >> (8 * umin((uint32_t)(off + 4 - csize), 3u))
+                                        : 0xFFFFFFFFu;
+    return in ? v & lo & hi : 0u;
 }
 
 // Stage src[s0 .. s0 + kStage) into LDS (src + s0 4-aligned; zero outside the input).
 __device__ __forceinline__ void stage_load(WaveLds &L, gcu8 *src, int csize, int s0,
                                            int lane) {
+    const int first = -(int)((uintptr_t)src & 3u);   // aligned dword holding byte 0
     uint32_t v[kStage / 256];
 #pragma unroll
-    for (int k = 0; k < kStage / 256; k++) v[k] = src_dword(src, csize, s0 + 4 * (lane + 64 * k));
+    for (int k = 0; k < kStage / 256; k++) v[k] = src_dword(src, csize, s0 + 4 * (lane + 64 * k), first);
 #pragma unroll
     for (int k = 0; k < kStage / 256; k++) *(uint32_t *)&L.stage[4 * (lane + 64 * k)] = v[k];
 }
@@ -514,14 +519,14 @@ __device__ __forceinline__ void lane_match(WaveLds &L, const Dec &D, uint32_t ba
         v2 = lds16(s + t2);
         v3 = lds16(s + t3);
     } else {
+        // all four loads issued together (t1..t3 are 0 for n <= 16: the same line again);
+        // with the last three under `n > 16` the first one's value was waited for before
+        // the others were issued
         gcu8 *s = (DICT && ps < 0) ? D.dend + ps : (gcu8 *)D.dst + ps;
         v0 = gload16_nt(s);
-        v1 = v2 = v3 = v0;
-        if (n > 16u) {
-            v1 = gload16_nt(s + t1);
-            v2 = gload16_nt(s + t2);
-            v3 = gload16_nt(s + t3);
-        }
+        v1 = gload16_nt(s + t1);
+        v2 = gload16_nt(s + t2);
+        v3 = gload16_nt(s + t3);
     }
     if (off == 0u) v0 = v1 = v2 = v3 = make_uint4(0, 0, 0, 0);
     if (big) {
