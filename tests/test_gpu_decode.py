@@ -112,6 +112,28 @@ def test_misaligned_buffers(cuda, product, oracle):
     assert outs == srcs
 
 
+def test_tiny_streams_every_alignment(cuda, product, oracle):
+    """Compressed blocks of 1-14 bytes (whole and cut short) at all 16 source alignments: the
+    staging loads read only dwords that intersect the block (a dword outside it re-reads the
+    one holding byte 0); return value and bytes bit-exact with the oracle."""
+    streams = []
+    for n in range(0, 10):
+        c = orc_compress(oracle, bytes(range(65, 65 + n)))[1]
+        streams += [c[:k] for k in range(1, len(c) + 1)]
+    comps, caps = [], []
+    for c in streams:
+        for cap in (16, 9):
+            comps.append(c)
+            caps.append(cap)
+    mis = [i % 16 for i in range(len(comps))]
+    rs, outs = run_decode(cuda, product, comps, caps, in_mis=mis, out_mis=[(3 * i) % 16 for i in range(len(comps))])
+    for c, cap, r, o in zip(comps, caps, rs, outs):
+        er, eo = orc_decompress(oracle, c, cap)
+        assert r == er, (c, cap, r, er)
+        if er > 0:
+            assert o == eo[:er]
+
+
 def test_blocks_beyond_64k(cuda, product, oracle):
     """The decoder has no block-size limit (only the 64 KiB offset window)."""
     srcs = [I.make("text", 70000), I.make("comp", 40000), I.make("rand", 200000, seed=3),
