@@ -734,7 +734,17 @@ def main():
         # no collective on the data path: the process group (gloo, host scalars) carries
         # only the barrier, the max-over-ranks time and the per-rank numbers
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        # gloo's C++ connect messages go to stdout; keep rank 0's stdout for the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     rc = amd.gpu_init()
     if rc != 0:
         raise SystemExit("GPU codec unavailable: %s" % amd.gpu_last_error())
