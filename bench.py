@@ -6,7 +6,11 @@ compress+decompress.  With --gpus N under torch.distributed.run the fixed batch 
 contiguously (rank r takes blocks [r*N_total/N, (r+1)*N_total/N), 131072 per GPU at N = 8;
 strong scaling, "scaling": "strong"), with no collective on the data path: a gloo process
 group carries the barrier, the max-over-ranks time and the per-rank numbers (`per_gpu`).
---weak gives every rank its own 1M blocks instead.
+--weak gives every rank its own 1M blocks instead.  `python bench.py --gpus N` starts the N
+ranks itself (one child process per GPU, before anything touches a GPU); under
+torch.distributed.run the launcher's WORLD_SIZE must equal --gpus.  Fewer than N visible
+devices is an error, unless APE_BENCH_DEVICE=d puts every rank on device d (a rehearsal of
+the N > 1 path on one GPU).
 
 One step = compress every block of the rank (one launch of lz4_encode_kernel) then
 decompress every compressed block (one launch of lz4_decode_kernel); inputs are generated
@@ -88,6 +92,9 @@ def host_cores():
         except OSError:
             pass
     info["model"] = model
+    if usable > 256:   # oracle/cpu_bench.c runs at most 256 threads
+        info["clamped_from"] = usable
+        usable = 256
     info["usable"] = usable
     return usable, info
 
@@ -673,6 +680,59 @@ def config2_leg(args, amd, torch, stream):
     }
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`--gpus N` without a launcher: start N ranks of this script (one process per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set) and exit with their status.
+    Nothing here touches a GPU (torch.cuda.device_count() does not initialise HIP on this
+    image), so the children start from a clean process.  Rank 0's stdout is this process's
+    stdout (the one JSON line); the other ranks' stdout goes to stderr."""
+    import signal
+
+    import torch
+
+    from libapenetwork_amd.sharding import launch_plan
+    try:
+        plan = launch_plan(args.gpus, args.blocks, torch.cuda.device_count(),
+                           os.environ.get("APE_BENCH_DEVICE"), args.weak, _free_port())
+    except ValueError as e:
+        log("bench.py: %s (set APE_BENCH_DEVICE=<id> to rehearse N ranks on one device)" % e)
+        return 2
+    procs = []
+    for p in plan:
+        env = dict(os.environ)
+        env.update(p["env"])
+        log("[launch] rank %d on device %d: blocks [%d, %d)" % (
+            p["rank"], p["device"], p["first_block"], p["first_block"] + p["nblocks"]))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] +
+                                      sys.argv[1:], env=env,
+                                      stdout=None if p["rank"] == 0 else sys.stderr.fileno()))
+    rc = 0
+    live = list(procs)
+    while live:
+        for pr in list(live):
+            code = pr.poll()
+            if code is None:
+                continue
+            live.remove(pr)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                log("bench.py: rank pid %d exited with %d; stopping the others" % (pr.pid, code))
+                for other in live:
+                    other.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.2)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -717,12 +777,23 @@ def main():
     if args.rand4k:
         return rand4k_bench(args)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args)
+
     import torch
 
     import libapenetwork_amd as amd
     from libapenetwork_amd.sharding import gather, reduce_max, reduce_sum, shard, shard_strong
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log("bench.py: --gpus %d but WORLD_SIZE=%d (the launcher's rank count)" % (args.gpus,
+                                                                                world))
+        return 2
+    if os.environ.get("APE_BENCH_DEVICE") is None and torch.cuda.device_count() < world:
+        log("bench.py: %d ranks but only %d device(s) visible" % (world,
+                                                                 torch.cuda.device_count()))
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # APE_BENCH_DEVICE (rehearsal only): every rank on that device, to exercise the N > 1
@@ -919,4 +990,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

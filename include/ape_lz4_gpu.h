@@ -135,12 +135,14 @@ int APE_LZ4_compress_destSize_batch_scratch_dev(const char *const *d_src, int *d
                                                 int *d_result, int nblocks, void *d_scratch,
                                                 size_t scratch_bytes, void *stream);
 
-/* One-shot routing (opt-in): ape_lz4.h one-shot calls on blocks smaller than `bytes`
- * (compress: input size; decompress_safe/_partial: capacity) run the host codec, which
- * is byte-identical to the reference; larger ones stay on the GPU.  Default 0 (all on
- * the GPU) or the APE_LZ4_ONESHOT_HOST_BELOW environment variable.  For callers whose
- * single calls are latency-bound (one GPU call costs 40-850 us, one host core 2-47 us
- * for 1-64 KiB).  Returns the previous threshold. */
+/* One-shot routing: ape_lz4.h one-shot calls on blocks smaller than
+ * `bytes` (compress: input size; decompress_safe/_partial: capacity) run the host codec,
+ * which is byte-identical to the reference; larger ones run on the GPU.  The default is
+ * 0x7FFFFFFF -- every one-shot call on the host, because one GPU call costs 40-850 us
+ * against 2-47 us on one host core for 1-64 KiB -- or the value of
+ * the APE_LZ4_ONESHOT_HOST_BELOW environment variable; 0 puts every one-shot call on the
+ * GPU.  The batch entry points below always run on the GPU.  Returns the previous
+ * threshold. */
 int APE_LZ4_gpu_set_oneshot_host_below(int bytes);
 
 /* ---- batched, device-resident, strided form (block i at base + i*stride) ----

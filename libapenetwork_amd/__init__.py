@@ -2,8 +2,9 @@
 
 The product is the C shared library ``libape_lz4_amd.so`` built next to this file
 (``make -C libapenetwork_amd/csrc``): it exports the reference's ape_lz4.h ABI
-(src/ape_lz4.h:59-467) with the one-shot block codec running as HIP kernels, and
-the batched device API of include/ape_lz4_gpu.h.  This module is a thin ctypes
+(src/ape_lz4.h:59-467) -- one-shot calls on its host codec by default,
+on HIP kernels when ``set_oneshot_host_below`` selects them -- and the batched device
+API of include/ape_lz4_gpu.h, whose codec is HIP kernels only.  This module is a thin ctypes
 mirror of that ABI for tests and the benchmark -- same function names, same
 argument meaning, same return conventions.  There is no Python or CPU fallback:
 importing works anywhere, but every call that needs the library raises if it is
@@ -20,7 +21,8 @@ __all__ = [
     "compress_prefix_batch", "decompress_dict_batch", "compress_fast_ptr_batch",
     "decompress_fast_ptr_batch", "compress_destSize_ptr_batch", "RxBuf",
     "compress_destSize_scratch_ptr_batch", "destSize_scratch_size",
-    "socket_send_blocks", "socket_recv_blocks",
+    "socket_send_blocks", "socket_recv_blocks", "set_oneshot_host_below", "oneshot_on_gpu",
+    "ONESHOT_HOST_ALL",
 ]
 
 _HERE = _os.path.dirname(_os.path.abspath(__file__))
@@ -28,6 +30,7 @@ _HERE = _os.path.dirname(_os.path.abspath(__file__))
 LIB_PATH = _os.environ.get("APE_LZ4_LIB") or _os.path.join(_HERE, "libape_lz4_amd.so")
 MAX_BLOCK = 65536
 ERANGE = -2147483648
+ONESHOT_HOST_ALL = 0x7FFFFFFF   # default one-shot threshold: every one-shot call on the host
 
 _lib = None
 
@@ -56,6 +59,7 @@ def lib():
             "APE_LZ4_gpu_init": (i, []),
             "APE_LZ4_gpu_device_count": (i, []),
             "APE_LZ4_gpu_last_error": (cp, []),
+            "APE_LZ4_gpu_set_oneshot_host_below": (i, [i]),
             "APE_LZ4_compress_batch_dev": (i, [p, p, p, p, p, i, p]),
             "APE_LZ4_compress_fast_batch_dev": (i, [p, p, p, p, p, i, i, p]),
             "APE_LZ4_compress_destSize_batch_dev": (i, [p, p, p, p, p, i, p]),
@@ -110,11 +114,29 @@ def gpu_last_error():
     return s.decode() if s else ""
 
 
+def set_oneshot_host_below(nbytes):
+    """APE_LZ4_gpu_set_oneshot_host_below: one-shot calls on blocks smaller than nbytes run
+    the host codec, larger ones the GPU (0 = all on the GPU).  Returns the previous value."""
+    return lib().APE_LZ4_gpu_set_oneshot_host_below(nbytes)
+
+
+class oneshot_on_gpu:
+    """Context manager: route every one-shot call to the GPU path inside the block."""
+
+    def __enter__(self):
+        self._prev = set_oneshot_host_below(0)
+        return self
+
+    def __exit__(self, *exc):
+        set_oneshot_host_below(self._prev)
+        return False
+
+
 def _buf(b, pad=16):
     return _C.create_string_buffer(bytes(b) + b"\0" * pad, len(b) + pad)
 
 
-# ---- one-shot ape_lz4.h calls (host buffers; GPU inside) ----
+# ---- one-shot ape_lz4.h calls (host buffers; host codec or GPU, see above) ----
 def compress_default(src, max_dst=None):
     """APE_LZ4_compress_default: returns (ret, compressed_bytes)."""
     cap = compressBound(len(src)) if max_dst is None else max_dst

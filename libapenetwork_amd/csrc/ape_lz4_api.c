@@ -2,7 +2,8 @@
  * ape_lz4_api.c -- the ape_lz4.h C ABI (all 40 symbols the reference exports,
  * ref src/ape_lz4.h:59-467 plus the 5 undeclared exports) for libape_lz4_amd.so.
  *
- *   one-shot block codec  -> MI355X HIP kernels through lz4_runtime.hip
+ *   one-shot block codec  -> host codec by default; MI355X HIP kernels through
+ *                            lz4_runtime.hip when APE_LZ4_ONESHOT_HOST_BELOW selects them
  *     compress_default / compress_fast / compress_fast_extState / compress /
  *     compress_limitedOutput / compress_withState / ..._withState /
  *     compress_fast_force, decompress_safe / decompress_safe_partial /
@@ -10,9 +11,10 @@
  *   chained streams, dictionaries, decompress_fast, destSize
  *     -> host stream codec (ape_lz4_host.c)
  *
- * There is no silent CPU fallback for the GPU entry points: without a usable
- * gfx950 device they report failure (0 from compress, -1 from decompress) and
- * print the runtime error once to stderr.
+ * One-shot calls run the product's host codec by default (see
+ * host_below() below); with the GPU one-shot path selected there is no silent CPU
+ * fallback: without a usable gfx950 device the calls report failure (0 from
+ * compress, -1 from decompress) and print the runtime error once to stderr.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -49,16 +51,18 @@ static int host_compress(void *state, const char *src, char *dst, int n, int cap
     return hst_compress_extstate(state ? (hst_stream *)state : &st, src, dst, n, cap, accel);
 }
 
-/* Opt-in latency routing ("a kernel launch costs more than one block").
- * One call of the GPU one-shot path is a pinned copy, H2D, one workgroup working through
- * the block's 1024 chunks, D2H and a stream sync: measured 39 / 126 / 848 us to compress
- * 1 / 8 / 64 KiB (decompress 45 / 112 / 784 us), against 5 / 6 / 47 us (2 / 3 / 15 us)
- * for the reference algorithm on one host core (tests/test_gpu_api.py).  The
- * GPU pays off only for many blocks at once -- the batch entry points.  The library's
- * contract stays "the codec runs on the GPU" (default threshold 0), so a missing GPU
- * fails loudly; a caller with single latency-bound blocks sets a threshold (API or
- * APE_LZ4_ONESHOT_HOST_BELOW), and one-shot calls on smaller blocks (compress: input
- * size; decompress: capacity) then run the host codec, byte-identical to the reference. */
+/* One-shot latency routing ("The single-block API stays on the CPU
+ * restatement, because a kernel launch costs more than one 8 KiB block").  One call of the
+ * GPU one-shot path is a pinned copy, H2D, one workgroup working through the block's 1024
+ * chunks, D2H and a stream sync: measured 39 / 126 / 848 us to compress 1 / 8 / 64 KiB
+ * (decompress 45 / 112 / 784 us), against 5 / 6 / 47 us (2 / 3 / 15 us) for the reference
+ * algorithm on one host core (tests/test_gpu_api.py).  So by default every
+ * one-shot call runs the product's host codec (ape_lz4_host.c), byte-identical to the
+ * reference; the GPU serves the batch entry points, which fail loudly without a device.
+ * A caller can move one-shot calls of blocks >= `bytes` to the GPU with
+ * APE_LZ4_gpu_set_oneshot_host_below(bytes) or APE_LZ4_ONESHOT_HOST_BELOW=bytes (0 = every
+ * one-shot call on the GPU; compress: input size, decompress: capacity). */
+#define ONESHOT_HOST_ALL 0x7FFFFFFF
 static int g_host_below = -1;
 
 static int host_below(void)
@@ -66,7 +70,7 @@ static int host_below(void)
     int v = __atomic_load_n(&g_host_below, __ATOMIC_RELAXED);
     if (v < 0) {
         const char *e = getenv("APE_LZ4_ONESHOT_HOST_BELOW");
-        v = e ? atoi(e) : 0;
+        v = (e && *e) ? atoi(e) : ONESHOT_HOST_ALL;
         if (v < 0) v = 0;
         __atomic_store_n(&g_host_below, v, __ATOMIC_RELAXED);
     }
@@ -99,7 +103,8 @@ static int gpu_compress(const char *src, char *dst, int n, int cap, int accel)
 static int gpu_decompress(const char *src, char *dst, int csize, int cap, int partial, int target)
 {
     int rt = 0, r;
-    if (cap >= 0 && cap < host_below())
+    const int hb = host_below();
+    if (hb == ONESHOT_HOST_ALL || (cap >= 0 && cap < hb))
         return hst_decompress_block(src, dst, csize, cap, partial, target);
     r = ape_lz4_gpu_decompress_one(src, dst, csize, cap, partial, target, &rt);
     if (rt) { gpu_failed(rt); return -1; }

@@ -1,6 +1,5 @@
 // lz4_encode.hip -- MI355X (gfx950) batched LZ4 block encoder: the product encoder.
-// (lz4_encode_v2.hip is a second pipeline, selected by APE_LZ4_ENCODER=v2 for A/B
-// measurement; DESIGN.md 3.1.1 says why it is not the default.)
+// (A second pipeline measured in round 2 lives only in the git history)
 //
 // Replaces the per-block work of APE_LZ4_compress_default (ref src/ape_lz4.c:
 // 811-815 -> LZ4_compress_generic :530-755, byU16 / noDict).  The output is a
@@ -46,13 +45,9 @@ namespace apelz4 {
 
 #ifdef APE_LZ4_STATS
 __device__ unsigned long long g_enc_stats[16];
-hipError_t enc_stats_v2_read(unsigned long long *out, int reset);
-// per-phase cycle sums of whichever encoder ran (the other one's are zero)
+// per-phase cycle sums of the encoder
 hipError_t enc_stats_read(unsigned long long *out, int reset) {
-    unsigned long long v2[16];
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_enc_stats), sizeof(g_enc_stats));
-    if (e == hipSuccess) e = enc_stats_v2_read(v2, reset);
-    for (int i = 0; i < 16 && e == hipSuccess; i++) out[i] += v2[i];
     if (e == hipSuccess && reset) {
         unsigned long long z[16] = {0};
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_enc_stats), z, sizeof(z));
@@ -60,8 +55,6 @@ hipError_t enc_stats_read(unsigned long long *out, int reset) {
     return e;
 }
 #endif
-
-hipError_t launch_encode_v2(const BlockArgs &a, hipStream_t s);
 
 namespace {
 
@@ -1188,12 +1181,6 @@ lz4_encode_kernel(BlockArgs a) {
 
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
-    // APE_LZ4_ENCODER=v2: the three-role v2 pipeline (lz4_encode_v2.hip), A/B only
-    static const int v2 = [] {
-        const char *e = getenv("APE_LZ4_ENCODER");
-        return e && e[0] == 'v' && e[1] == '2' ? 1 : 0;
-    }();
-    if (v2 && a.accel <= 1) return launch_encode_v2(a, s);
     if (a.accel > 1)
         hipLaunchKernelGGL(lz4_encode_kernel<true>, dim3(a.nblocks), dim3(192), 0, s, a);
     else

@@ -151,7 +151,6 @@ hipError_t launch_destsize(const char *const *src, int *src_size, char *const *d
 hipError_t launch_frame_offsets(const int *csize, long long *off, long long *scratch, int n,
                                 hipStream_t s);
 int frame_scratch_elems(int n);
-bool gpu_probed();   // the runtime's device probe ran and found a device
 hipError_t launch_frame_pack(const char *comp, size_t stride, const int *csize,
                              const long long *off, char *frames, int n, hipStream_t s);
 hipError_t launch_synth(char *out, size_t stride, int n, long long first, int nblocks,

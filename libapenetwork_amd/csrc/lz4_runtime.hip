@@ -190,6 +190,9 @@ int host_batch(int mode, int accel, const char *const *h_src, const int *h_in, c
     if (rc) { ctx_return(ctx); return rc; }
     rc = host_batch_run(*ctx, mode, accel, h_src, h_in, h_dst, h_cap, h_target, h_res, nb,
                         in_off, out_off, out_len, total);
+    // a failed run may have left copies or the kernel queued on the context's stream:
+    // drain them before another caller can borrow its pinned buffer
+    if (rc) (void)hipStreamSynchronize(ctx->stream);
     ctx_return(ctx);
     return rc;
 }
@@ -258,7 +261,6 @@ BlockArgs ptr_args(const char *const *src, const int *in, char *const *dst, cons
 }  // namespace
 
 // the device probe already ran and found a device (never triggers the probe itself)
-bool apelz4::gpu_probed() { return g_ndev > 0; }
 
 extern "C" {
 

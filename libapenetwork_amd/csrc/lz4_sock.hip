@@ -271,7 +271,8 @@ long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_strid
 // APE_LZ4_GPU_E* code (APE_LZ4_GPU_EINVAL also for a malformed frame or early EOF).
 long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int block_size,
                                      int nblocks, int batch, int *h_result) {
-    if (fd < 0 || !h_dst || !h_result || block_size <= 0 || nblocks < 0 || batch <= 0 ||
+    if (fd < 0 || !h_dst || !h_result || block_size <= 0 || block_size > kMaxBlock ||
+        nblocks < 0 || batch <= 0 ||
         dst_stride < (size_t)block_size)
         return APE_LZ4_GPU_EINVAL;
     int rc = APE_LZ4_gpu_init();

@@ -21,6 +21,31 @@ def shard_strong(rank, world, total_blocks):
     return first, (rank + 1) * total_blocks // world - first
 
 
+def launch_plan(ngpus, total_blocks, device_count, rehearsal_device=None, weak=False,
+                master_port=29500):
+    """The ranks `bench.py --gpus N` starts by itself (one process per GPU):
+    a list of {rank, device, first_block, nblocks, env} with the RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* environment of each child.  Raises ValueError when fewer than N
+    devices are visible, unless `rehearsal_device` (APE_BENCH_DEVICE) puts every rank on
+    that one device."""
+    if ngpus < 1:
+        raise ValueError("--gpus must be >= 1, got %r" % (ngpus,))
+    if rehearsal_device is None and device_count < ngpus:
+        raise ValueError("--gpus %d but only %d device(s) visible" % (ngpus, device_count))
+    plan = []
+    for r in range(ngpus):
+        first, nb = shard(r, ngpus, total_blocks) if weak else shard_strong(r, ngpus,
+                                                                            total_blocks)
+        plan.append({
+            "rank": r, "device": r if rehearsal_device is None else int(rehearsal_device),
+            "first_block": first, "nblocks": nb,
+            "env": {"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(ngpus),
+                    "LOCAL_WORLD_SIZE": str(ngpus), "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": str(master_port)},
+        })
+    return plan
+
+
 def shard(rank, world, blocks_per_rank):
     """(first_block, nblocks) of `rank` in a weak-scaled batch of world*blocks_per_rank."""
     if world < 1 or not 0 <= rank < world or blocks_per_rank < 0:

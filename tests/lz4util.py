@@ -2,8 +2,21 @@
 import base64
 import ctypes as C
 import hashlib
+import os
 
 import inputs as I
+
+_REF = []
+
+
+def ref_lib():
+    """oracle/_ref/libape_lz4_ref.so -- the reference src/ape_lz4.c compiled from its own
+    source by oracle/Makefile (a checker, like the oracle), or None when it was not built."""
+    if not _REF:
+        p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         "oracle", "_ref", "libape_lz4_ref.so")
+        _REF.append(C.CDLL(p) if os.path.exists(p) else None)
+    return _REF[0]
 
 
 def buf(b, pad=64):

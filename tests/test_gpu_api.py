@@ -1,6 +1,7 @@
 """The drop-in ape_lz4.h one-shot calls on a real MI355X (host buffers in and out,
 pinned staging + H2D/D2H inside the library), plus the host-buffer batch API and the
-device-side benchmark generator.
+device-side benchmark generator.  One-shot calls run the host codec by default (SURVEY
+8(b)); the tests of the GPU one-shot path select it with the `gpu_oneshot` fixture.
 """
 import base64
 import ctypes as C
@@ -13,7 +14,14 @@ from lz4util import I, buf, orc_compress, orc_decompress, sha
 pytestmark = pytest.mark.gpu
 
 
-def test_one_shot_decompress_matches_reference_kats(cuda, product, golden):
+@pytest.fixture
+def gpu_oneshot(product):
+    """Every one-shot call on the GPU path for the test (threshold 0), default after."""
+    with product.oneshot_on_gpu():
+        yield
+
+
+def test_one_shot_decompress_matches_reference_kats(cuda, product, golden, gpu_oneshot):
     for d in golden["decode"][::3]:
         comp = base64.b64decode(d["comp_b64"])
         r, out = product.decompress_safe(comp, d["cap"])
@@ -24,7 +32,7 @@ def test_one_shot_decompress_matches_reference_kats(cuda, product, golden):
         assert pr == d["partial"]["ret"], d["name"]
 
 
-def test_one_shot_compress_roundtrip(cuda, product, oracle):
+def test_one_shot_compress_roundtrip(cuda, product, oracle, gpu_oneshot):
     rng = random.Random(3)
     L = product.lib()
     for i in range(40):
@@ -91,7 +99,7 @@ def test_device_generator_matches_spec(cuda, product, oracle):
             assert h[b, :n].tobytes() == fn(n, 1000 + b)
 
 
-def test_concurrent_one_shot_callers(cuda, product, oracle):
+def test_concurrent_one_shot_callers(cuda, product, oracle, gpu_oneshot):
     """SURVEY 8(b) threading: the shim is thread-safe per call.  8 threads issue one-shot
     compress_default / decompress_safe / decompress_safe_partial calls at once (ctypes drops
     the GIL around each call); every result must equal the single-threaded one."""
@@ -137,36 +145,77 @@ def test_concurrent_one_shot_callers(cuda, product, oracle):
 
 
 def test_one_shot_latency_recorded(cuda, product, oracle):
-    """One-call latency of the GPU one-shot path next to the reference algorithm on one
-    host core (the oracle restatement, as the checker's clock), for the routing note in
-    DESIGN.md: printed, and sanity-bounded only."""
+    """One-call latency of the one-shot calls, by default (host codec) and on
+    the GPU path (threshold 0), next to the reference algorithm on one host core (the oracle
+    restatement, as the checker's clock): printed for DESIGN.md section 1; the default must
+    be no slower than the host core and return the same bytes."""
     import time
     L = product.lib()
+
+    def clock(fn, reps=20):
+        for _ in range(3):
+            fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = fn()
+        return (time.perf_counter() - t0) / reps, r
+
     for n in (1024, 8192, 65536):
         s = I.make("comp", n, seed=5)
-        o = C.create_string_buffer(product.compressBound(n) + 64)
+        bound = product.compressBound(n)
         b = buf(s)
-        for _ in range(3):
-            L.APE_LZ4_compress_default(b, o, n, product.compressBound(n))
-        t0 = time.perf_counter()
-        for _ in range(20):
-            r = L.APE_LZ4_compress_default(b, o, n, product.compressBound(n))
-        dt = (time.perf_counter() - t0) / 20
+        o = C.create_string_buffer(bound + 64)
+        dt, r = clock(lambda: L.APE_LZ4_compress_default(b, o, n, bound))
+        comp = o.raw[:r]
+        er, ecomp = orc_compress(oracle, s)
+        assert r == er and comp == ecomp           # the host codec = the reference's bytes
+        cb = buf(comp)
         d = C.create_string_buffer(n + 64)
-        cb = buf(o.raw[:r])
-        t0 = time.perf_counter()
-        for _ in range(20):
-            L.APE_LZ4_decompress_safe(cb, d, r, n)
-        dd = (time.perf_counter() - t0) / 20
-        t0 = time.perf_counter()
-        for _ in range(20):
-            orc_compress(oracle, s)
-        hc = (time.perf_counter() - t0) / 20
-        t0 = time.perf_counter()
-        for _ in range(20):
-            orc_decompress(oracle, o.raw[:r], n)
-        hd = (time.perf_counter() - t0) / 20
-        print("one-shot n=%d: GPU compress %.1f us, decompress %.1f us | one host core "
-              "(reference algorithm): compress %.1f us, decompress %.1f us" % (
-                  n, dt * 1e6, dd * 1e6, hc * 1e6, hd * 1e6))
-        assert dt < 0.5 and dd < 0.5
+        dd, r2 = clock(lambda: L.APE_LZ4_decompress_safe(cb, d, r, n))
+        assert r2 == n and d.raw[:n] == s
+        with product.oneshot_on_gpu():
+            gdt, gr = clock(lambda: L.APE_LZ4_compress_default(b, o, n, bound))
+            assert gr > 0
+            gcb = buf(o.raw[:gr])
+            gdd, gr2 = clock(lambda: L.APE_LZ4_decompress_safe(gcb, d, gr, n))
+            assert gr2 == n and d.raw[:n] == s
+        # one host core, the restatement called with preallocated buffers
+        ob = C.create_string_buffer(bound + 64)
+        hc, _ = clock(lambda: oracle.orc_compress_default(b, ob, n, bound))
+        hd, _ = clock(lambda: oracle.orc_decompress_safe(cb, d, r, n))
+        print("one-shot n=%d: default (host codec) compress %.1f us, decompress %.1f us | GPU "
+              "path compress %.1f us, decompress %.1f us | one host core (reference algorithm): "
+              "compress %.1f us, decompress %.1f us" % (
+                  n, dt * 1e6, dd * 1e6, gdt * 1e6, gdd * 1e6, hc * 1e6, hd * 1e6))
+        assert dt <= 1.25 * hc + 2e-6 and dd <= 1.25 * hd + 2e-6
+        assert gdt < 0.5 and gdd < 0.5
+
+
+def test_host_batch_decode_huge_caps(cuda, product, golden, oracle):
+    """host-buffer batch decode stages at most min(cap, 255 csize + 64) bytes per
+    block while the kernel sees the caller's cap; with caps far above what a block can
+    expand to, valid, mutated and truncated blocks return exactly the oracle's results."""
+    import base64
+    L = product.lib()
+    rng = random.Random(11)
+    blobs = [base64.b64decode(d["comp_b64"]) for d in golden["decode"]][:40]
+    for i in range(20):
+        _, c = orc_compress(oracle, I.make("comp", rng.randrange(1, 4000), seed=i))
+        c = bytearray(c)
+        if i % 2:
+            c[rng.randrange(len(c))] = rng.randrange(256)
+        blobs.append(bytes(c[:rng.randrange(1, len(c) + 1)] if i % 3 == 0 else c))
+    cap = (1 << 20) + 3
+    nb = len(blobs)
+    keep = [buf(b) for b in blobs]
+    outs = [C.create_string_buffer(cap + 64) for _ in blobs]
+    res = (C.c_int * nb)()
+    rc = L.APE_LZ4_decompress_safe_batch_host(
+        (C.c_void_p * nb)(*[C.addressof(k) for k in keep]), (C.c_int * nb)(*map(len, blobs)),
+        (C.c_void_p * nb)(*[C.addressof(o) for o in outs]), (C.c_int * nb)(*([cap] * nb)), res, nb)
+    assert rc == 0
+    for i, b in enumerate(blobs):
+        er, eout = orc_decompress(oracle, b, cap)
+        assert res[i] == er, i
+        if er > 0 and not (i < 40 and golden["decode"][i]["has_offset0"]):
+            assert outs[i].raw[:er] == eout, i

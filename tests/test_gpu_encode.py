@@ -1,17 +1,21 @@
 """GPU encoder: emits valid LZ4 v1.7.1 blocks.
 
-Bar (north_star): the reference decompress_safe (the oracle restatement, pinned to
-the reference by tests/test_oracle_golden.py) restores the input exactly with
-cap = srcSize, the output never exceeds compressBound, limited-output semantics
-hold (0 when it does not fit), output is deterministic, and the compression
-ratio on the benchmark data is reported next to the reference's.
+Bar (north_star): "a valid LZ4 block that the reference decompresses to the original
+bytes" -- every GPU-compressed block is decoded by the reference ITSELF (oracle/_ref, the
+reference src/ape_lz4.c compiled from its own source, when present: always on the GPU box)
+and by the oracle restatement (pinned to the reference by tests/test_oracle_golden.py):
+cap = srcSize restores the input exactly, cap = srcSize - 1 fails with the same return
+code in both; the output never exceeds compressBound, limited-output semantics hold (0 when
+it does not fit), output is deterministic, and the compression ratio on the benchmark data
+is reported next to the reference's.
 """
+import ctypes as C
 import random
 
 import pytest
 
 from gpuutil import alloc_out, fetch, ints, pack
-from lz4util import I, orc_compress, orc_decompress, walk_ok
+from lz4util import I, buf, orc_compress, orc_decompress, ref_lib, walk_ok
 
 pytestmark = pytest.mark.gpu
 
@@ -33,11 +37,47 @@ def run_encode(torch, amd, srcs, caps=None, in_mis=None, out_mis=None):
     return rs, [fetch(dst, o, r) for o, r in zip(doffs, rs)]
 
 
+def ref_decode(ref, comp, cap):
+    """APE_LZ4_decompress_safe of the reference library itself: (ret, dst[0:ret])."""
+    o = C.create_string_buffer(max(cap, 0) + 64)
+    r = ref.APE_LZ4_decompress_safe(buf(comp), o, len(comp), cap)
+    return r, o.raw[:max(r, 0)]
+
+
 def check_valid(oracle, src, comp):
-    r, out = orc_decompress(oracle, comp, len(src))
-    assert r == len(src), (len(src), r)
+    n = len(src)
+    r, out = orc_decompress(oracle, comp, n)
+    assert r == n, (n, r)
     assert out == src
     walk_ok(comp)  # parses as a well-formed sequence list
+    ref = ref_lib()
+    if ref is not None:   # the reference decoder itself (oracle/_ref)
+        assert ref_decode(ref, comp, n) == (n, src), n
+        if n > 0:         # one byte short: a decode error, the same one in both
+            rr, _ = ref_decode(ref, comp, n - 1)
+            assert rr < 0 and rr == orc_decompress(oracle, comp, n - 1)[0], (n, rr)
+
+
+def test_encoder_output_decoded_by_reference_itself(cuda, product, oracle):
+    """the config-3 sample (64 x 64 KiB App. C blocks) plus 4 KiB random
+    and compressible blocks and the edge sizes, compressed on the GPU, decoded by the
+    reference library itself (cap = n: the input; cap = n - 1: the same error as the
+    oracle's)."""
+    if ref_lib() is None:
+        pytest.skip("oracle/_ref (the reference built from its own source) not present")
+    srcs = [I.synth_comp(65536, b) for b in range(64)] + \
+           [I.synth_rand(4096, b) for b in range(64)] + \
+           [I.synth_comp(4096, b) for b in range(64)] + \
+           [I.make(c, n, seed=n) for c in ("comp", "text", "zeros", "rand")
+            for n in (0, 1, 12, 13, 14, 15, 16, 17, 100, 4095, 65535, 65536)]
+    rs, comps = run_encode(cuda, product, srcs)
+    ref = ref_lib()
+    for s, r, c in zip(srcs, rs, comps):
+        assert 0 < r <= product.compressBound(len(s))
+        assert ref_decode(ref, c, len(s)) == (len(s), s), len(s)
+        if len(s):
+            rr, _ = ref_decode(ref, c, len(s) - 1)
+            assert rr < 0 and rr == orc_decompress(oracle, c, len(s) - 1)[0]
 
 
 def test_golden_inputs_roundtrip(cuda, product, oracle):

@@ -132,3 +132,52 @@ def test_two_rank_gloo(oracle):
         assert tot_comp == total and tot_ok == WORLD
         assert [(f, c) for f, c, _ in ranges] == [(0, 6), (6, 7)]   # disjoint, covering
         assert [ck for _, _, cks in ranges for ck in cks] == all_cks
+
+
+def test_launch_plan_for_gpus_flag():
+    """`bench.py --gpus N` (no torchrun) starts N ranks itself: one per device, each with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* and its contiguous shard."""
+    from libapenetwork_amd.sharding import launch_plan
+    for n in (2, 8):
+        plan = launch_plan(n, 1 << 20, device_count=8, master_port=12345)
+        assert [p["rank"] for p in plan] == list(range(n))
+        assert [p["device"] for p in plan] == list(range(n))
+        assert [p["nblocks"] for p in plan] == [(1 << 20) // n] * n
+        assert [p["first_block"] for p in plan] == [r * ((1 << 20) // n) for r in range(n)]
+        for p in plan:
+            e = p["env"]
+            assert e["RANK"] == e["LOCAL_RANK"] == str(p["rank"])
+            assert e["WORLD_SIZE"] == str(n) and e["MASTER_ADDR"] == "127.0.0.1"
+            assert e["MASTER_PORT"] == "12345"
+    assert launch_plan(8, 1 << 20, 8)[7]["nblocks"] == 131072
+    # weak scaling: every rank its own --blocks
+    assert [(p["first_block"], p["nblocks"]) for p in launch_plan(2, 10, 2, weak=True)] == \
+        [(0, 10), (10, 10)]
+    # too few devices is an error, unless a rehearsal device is named
+    with pytest.raises(ValueError):
+        launch_plan(8, 1 << 20, device_count=1)
+    plan = launch_plan(2, 131072, device_count=1, rehearsal_device="0")
+    assert [p["device"] for p in plan] == [0, 0]
+    assert [p["nblocks"] for p in plan] == [65536, 65536]
+
+
+def _bench(args, env_extra):
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("APE_BENCH_DEVICE", None)
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=300)
+
+
+def test_bench_refuses_to_misreport_world_size():
+    """bench.py exits non-zero instead of timing one GPU and printing n_gpus: 1 when --gpus
+    and the launcher's world size disagree, or when fewer devices than --gpus are visible."""
+    import torch
+    r = _bench(["--gpus", "1"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr and r.stdout == ""
+    if torch.cuda.device_count() < 2:
+        r = _bench(["--gpus", "2"], {})
+        assert r.returncode == 2 and "device(s) visible" in r.stderr and r.stdout == ""

@@ -5,7 +5,8 @@
 * the host stream codec (the socket TX/RX path) is bit-exact
   with the reference on the golden stream KATs and with the oracle on dictionary /
   prefix / fast decoding;
-* without a GPU the one-shot GPU entry points fail loudly (no CPU fallback).
+* one-shot calls run the host codec by default; with the GPU one-shot path
+  selected, and for every batch entry point, no GPU means a loud failure (no CPU fallback).
 """
 import base64
 import ctypes as C
@@ -179,16 +180,24 @@ def test_host_dict_and_fast_decoders_vs_oracle(product, oracle):
 
 
 def test_no_gpu_fails_loudly(product):
-    """Without a device the GPU entry points report failure; nothing falls back to CPU."""
+    """Without a device the GPU entry points report failure; nothing falls back to CPU.
+    One-shot calls take the host codec by default; once the GPU one-shot
+    path is selected they fail too."""
     L = product.lib()
     if L.APE_LZ4_gpu_device_count() > 0:
         pytest.skip("a GPU is visible here; covered by the -m gpu suite")
     assert product.gpu_init() == -1
     assert "no HIP device" in product.gpu_last_error()
-    r, _ = product.compress_default(b"hello hello hello hello hello")
-    assert r == 0
-    r, _ = product.decompress_safe(b"\x50hello", 5)
-    assert r < 0
+    r, comp = product.compress_default(b"hello hello hello hello hello")   # default: host
+    assert r > 0 and product.decompress_safe(comp, 29) == (29, b"hello hello hello hello hello")
+    with product.oneshot_on_gpu():
+        r, _ = product.compress_default(b"hello hello hello hello hello")
+        assert r == 0
+        r, _ = product.decompress_safe(b"\x50hello", 5)
+        assert r < 0
+    # the batch API has no host path at all
+    z = C.c_void_p(0)
+    assert L.APE_LZ4_compress_batch_dev(z, z, z, z, z, 1, z) != 0
 
 
 def test_one_shot_compress_above_gpu_block(product, golden, oracle):
@@ -229,10 +238,10 @@ def test_one_shot_compress_above_gpu_block(product, golden, oracle):
 
 
 def test_oneshot_host_routing_threshold(product, golden):
-    """APE_LZ4_gpu_set_oneshot_host_below (opt-in latency routing): below the
+    """APE_LZ4_gpu_set_oneshot_host_below (latency routing): below the
     threshold the one-shot calls run the host codec and return the reference's exact
     results -- compress bytes, decompress_safe and _partial return values and bytes --
-    GPU or not; the default (0) keeps every one-shot call on the GPU."""
+    GPU or not; the default (0x7FFFFFFF) keeps every one-shot call on the host."""
     import base64
     from lz4util import blob_matches
     L = product.lib()
@@ -240,7 +249,7 @@ def test_oneshot_host_routing_threshold(product, golden):
     L.APE_LZ4_gpu_set_oneshot_host_below.argtypes = [C.c_int]
     prev = L.APE_LZ4_gpu_set_oneshot_host_below(1 << 30)
     try:
-        assert prev == 0
+        assert prev == product.ONESHOT_HOST_ALL
         for e in golden["encode"]:
             if e["n"] > 65536:
                 continue
@@ -258,5 +267,6 @@ def test_oneshot_host_routing_threshold(product, golden):
             assert pr == d["partial"]["ret"], d["name"]
     finally:
         assert L.APE_LZ4_gpu_set_oneshot_host_below(prev) == 1 << 30
-    if L.APE_LZ4_gpu_device_count() == 0:   # back on the GPU path: fails loudly here
-        assert product.compress_default(b"hello hello hello hello hello")[0] == 0
+    if L.APE_LZ4_gpu_device_count() == 0:   # the GPU one-shot path fails loudly here
+        with product.oneshot_on_gpu():
+            assert product.compress_default(b"hello hello hello hello hello")[0] == 0
