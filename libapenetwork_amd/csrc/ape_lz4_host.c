@@ -86,7 +86,11 @@ static inline const byte *vaddr(const cctx *c, uintptr_t v)
     return c->src + (v - c->cur);
 }
 
-static int compress_core(hst_stream *st, const byte *src, byte *dst, int n, int cap,
+/* always inlined: every caller passes its table/dict/limited mode as constants, so each
+ * call site compiles to a specialised loop, as the reference's LZ4_FORCE_INLINE
+ * LZ4_compress_generic does (ref :530) -- the generic loop was ~45 % slower */
+static inline __attribute__((always_inline))
+int compress_core(hst_stream *st, const byte *src, byte *dst, int n, int cap,
                          int limited, int tbl, int dict, int small, unsigned accel)
 {
     cctx c;
@@ -141,7 +145,15 @@ static int compress_core(hst_stream *st, const byte *src, byte *dst, int n, int 
             if (limited && op + lit + 8 + lit / 255 > oend) return 0;
             if (lit >= 15) { *tok = 15 << 4; op = put_run(op, lit - 15); }
             else *tok = (byte)(lit << 4);
-            memcpy(op, anchor, lit);
+            {   /* 8-byte units (the reference's wildCopy, :646): at most 7 bytes past
+                   op + lit, which stay below the end of dst -- limited mode checked
+                   op + lit + 8 <= oend above; otherwise an offset, the last token and
+                   >= 5 last literals still follow within cap -- and reads stay below
+                   ip + 8 <= iend - 4 (ip <= mflimit) */
+                byte *d = op;
+                const byte *q = anchor;
+                do { copy8(d, q); d += 8; q += 8; } while (d < op + lit);
+            }
             op += lit;
         }
         for (;;) {  /* match (:652-698), possibly repeated (:709-726) */
@@ -310,7 +322,9 @@ tail: {
  * low = first byte a match may reference (dest - prefix); with ext dict,
  * offsets reaching below `low` continue into [dstart, dstart + dsize).
  * ------------------------------------------------------------------------ */
-static int decode_core(const byte *src, byte *dst, int isize, int osize, int safe, int partial,
+/* always inlined per call site, like LZ4_decompress_generic (ref :1275) */
+static inline __attribute__((always_inline))
+int decode_core(const byte *src, byte *dst, int isize, int osize, int safe, int partial,
                        int target, int ext, const byte *low, const byte *dstart, size_t dsize)
 {
     static const int inc32[8] = {4, 1, 2, 1, 4, 4, 4, 4};
@@ -447,8 +461,15 @@ int hst_compress_extstate(hst_stream *s, const char *src, char *dst, int n, int 
     const int bound = (uint32_t)n > (uint32_t)HST_MAX_INPUT ? 0 : n + n / 255 + 16;
     hst_reset(s);
     if (accel < 1) accel = 1;
-    return compress_core(s, (const byte *)src, (byte *)dst, n, cap, cap < bound,
-                         n < HST_LIMIT64K ? TBL_U16 : TBL_U32, DICT_NONE, 0, (unsigned)accel);
+    if (n < HST_LIMIT64K) {
+        if (cap < bound)
+            return compress_core(s, (const byte *)src, (byte *)dst, n, cap, 1, TBL_U16,
+                                 DICT_NONE, 0, (unsigned)accel);
+        return compress_core(s, (const byte *)src, (byte *)dst, n, cap, 0, TBL_U16, DICT_NONE,
+                             0, (unsigned)accel);
+    }
+    return compress_core(s, (const byte *)src, (byte *)dst, n, cap, cap < bound, TBL_U32,
+                         DICT_NONE, 0, (unsigned)accel);
 }
 
 int hst_compress_force(const char *src, char *dst, int n, int cap, int accel)
@@ -578,8 +599,11 @@ int hst_decompress_safe_extdict(const char *s, char *d, int csize, int cap, cons
 /* decompress_safe / _safe_partial of one block without a dictionary (ref :1472-1487) */
 int hst_decompress_block(const char *s, char *d, int csize, int cap, int partial, int target)
 {
-    return decode_core((const byte *)s, (byte *)d, csize, cap, 1, partial, target, 0,
-                       (const byte *)d, NULL, 0);
+    if (partial)
+        return decode_core((const byte *)s, (byte *)d, csize, cap, 1, 1, target, 0,
+                           (const byte *)d, NULL, 0);
+    return decode_core((const byte *)s, (byte *)d, csize, cap, 1, 0, 0, 0, (const byte *)d,
+                       NULL, 0);
 }
 
 int hst_decompress_usingDict(const char *s, char *d, int csize, int cap, int safe,

@@ -214,9 +214,12 @@ def test_acceleration(cuda, product, oracle):
     # a huge acceleration probes only the three positions after each match end (and the
     # block's first three): little is found, but the blocks stay valid (checked above)
     assert ratio[1 << 30] < 1.5
-    # the one-shot API routes acceleration too
-    r, c = product.compress_fast(srcs[0], acceleration=4)
+    # the one-shot API routes acceleration too: the GPU path gives the batch's bytes, the
+    # default (host codec) the reference's own
+    with product.oneshot_on_gpu():
+        r, c = product.compress_fast(srcs[0], acceleration=4)
     assert c == out[4][1][0]
+    assert product.compress_fast(srcs[0], acceleration=4) == orc_compress(oracle, srcs[0], accel=4)
 
 
 def test_destsize(cuda, product, oracle):
