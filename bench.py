@@ -131,12 +131,15 @@ def _sweep_threads(usable):
     return ts + [usable]
 
 
-def cpu_baseline(block, kind, nblocks, mode=0):
+def cpu_baseline(block, kind, nblocks, mode=0, min_seconds=0.0, repeats=1):
     """The reference codec on this host's cores: one block per
     task, static partition, a 1..N thread sweep, gcc and clang builds.  mode 0 =
     compress_default + decompress_safe (config 3), 1 = decompress_safe only (config 2).
-    The sample is generated and compressed once untimed; each sweep point times one
-    full pass over it (after a warm-up pass) and checks every decoded block."""
+    The sample is generated and compressed once untimed; each sweep point times whole
+    passes over it (after a warm-up pass) and checks every decoded block.  With
+    min_seconds, a measurement repeats the pass until it lasts that long (a 1 GiB config-2
+    pass takes ~10 ms on 16 cores: too short to time alone), and the sweep point is the
+    median of `repeats` such measurements."""
     usable, cores = host_cores()
     lib = _cpubench()
     out = (C.c_double * 5)()
@@ -149,19 +152,32 @@ def cpu_baseline(block, kind, nblocks, mode=0):
             return None
         try:
             for t in threads:
-                if lib.cpu_bench_time(h, t, 1, mode, out) != 0 or out[3] != 0:
-                    return None
-                tc, td, csz, byt = out[0], out[1], out[2], out[4]
+                reps = 1
+                if min_seconds > 0:   # size the repetition count from one pass
+                    if lib.cpu_bench_time(h, t, 1, mode, out) != 0 or out[3] != 0:
+                        return None
+                    reps = max(1, int(min_seconds / max(out[0] + out[1], 1e-6)) + 1)
+                meas = []
+                for _ in range(max(1, repeats)):
+                    if lib.cpu_bench_time(h, t, reps, mode, out) != 0 or out[3] != 0:
+                        return None
+                    meas.append((out[4] * reps / (out[0] + out[1]), out[0], out[1]))
+                meas.sort()
+                med = meas[len(meas) // 2]
+                tc, td, csz, byt = med[1], med[2], out[2], out[4] * reps
                 v = byt / (tc + td) / GIB
                 row = next((r for r in sweep if r["threads"] == t), None)
                 if row is None:
                     row = {"threads": t}
                     sweep.append(row)
                 row[label] = round(v, 3)
+                if repeats > 1:
+                    row.setdefault("spread_" + label, [round(m[0] / GIB, 3) for m in meas])
+                    row["reps"] = reps
                 if t == usable:
                     split[label] = {"value": round(v, 3),
                                     "decompress_GiBps": round(byt / td / GIB, 3),
-                                    "ratio": round(byt / csz, 4)}
+                                    "ratio": round(out[4] / csz, 4)}
                     if mode == 0:
                         split[label]["compress_GiBps"] = round(byt / tc / GIB, 3)
                     if best is None or v > best[1]:
@@ -174,9 +190,11 @@ def cpu_baseline(block, kind, nblocks, mode=0):
         "value": round(v, 3), "unit": "GiB/s", "cores": usable, "kind": kindname,
         "compiler": label,
         "sample": "%d x %d KiB %s blocks (%.2f GiB), %s, one block per task, static partition "
-                  "over %d threads; best of %s at %d threads" % (
+                  "over %d threads; best of %s at %d threads%s" % (
                       nblocks, block >> 10, "compressible" if kind else "random",
-                      nblocks * block / GIB, what, usable, "/".join(split), usable),
+                      nblocks * block / GIB, what, usable, "/".join(split), usable,
+                      (", each sweep point the median of %d measurements of >= %.1f s" % (
+                          repeats, min_seconds)) if repeats > 1 else ""),
         "host": cores, "sweep": sweep, "by_compiler": split,
     }
     res.update({k: v2 for k, v2 in split[label].items() if k != "value"})
@@ -952,7 +970,8 @@ def main():
         torch.cuda.empty_cache()
         c2 = config2_leg(args, amd, torch, stream)
         if not args.no_cpu_baseline:
-            c2["cpu_baseline"] = cpu_baseline(4096, 0, args.config2_blocks, mode=1)
+            c2["cpu_baseline"] = cpu_baseline(4096, 0, args.config2_blocks, mode=1,
+                                              min_seconds=1.0, repeats=3)
 
     c5 = None
     if rank == 0 and world == 1 and not args.no_config5:

@@ -9,10 +9,11 @@
 // not by the reference's sequential search, so the bytes differ.
 //
 // One 192-thread workgroup (three waves, one role each) per block; a batch holds
-// ~1M blocks, so most of the parallelism comes from many blocks in flight (8 per
-// CU).  Per block the LDS (19.9 KiB) holds the reference's own hash table (8192 x
-// u16, 13-bit hash of 5 bytes, :449-462), a 1 KiB ring of recent input and the
-// hand-over records between the roles.  The input stays in HBM/L2.
+// ~1M blocks, so most of the parallelism comes from many blocks in flight (9 per
+// CU).  Per block the LDS (17.4 KiB) holds a hash table like the reference's (:449-462:
+// u16 positions, a hash of 5 bytes; 6912 entries instead of 8192, see kHSize), a 1 KiB
+// ring of recent input and the hand-over records between the roles.  The input stays in
+// HBM/L2.
 //
 // The block is cut into chunks of 64 positions, one per lane.  The waves run in
 // lock step, two workgroup barriers per step s (each waits only on its own memory
@@ -62,12 +63,24 @@ namespace {
 #define APE_LZ4_HLOG 13
 #endif
 constexpr int kHLog = APE_LZ4_HLOG;
-constexpr int kHSize = 1 << kHLog;
+// Table entries.  The reference's 8192 (2^13) entries make the block's LDS 20.4 KiB, so
+// 8 blocks fit a CU; 6912 entries (the 13-bit hash scaled onto [0, 6912)) make it 17.4 KiB,
+// inside the 17.5 KiB (35 x 512-byte LDS granules) that fits 9 blocks = 27 waves per CU
+// (7 per SIMD: <= 72 VGPRs).  Measured on 131072 blocks: encode -4.6 %, ratio 3.1464 ->
+// 3.1279 (tools/enc_model.c models the ratio per table size).
+#ifndef APE_LZ4_TSIZE
+#define APE_LZ4_TSIZE 6912
+#endif
+constexpr int kHSize = APE_LZ4_TSIZE;
+static_assert(kHSize <= (1 << kHLog) && kHSize % 8 == 0, "table size");
+#ifndef APE_LZ4_WAVES_PER_EU
+#define APE_LZ4_WAVES_PER_EU 7
+#endif
 #ifndef APE_LZ4_EAGER_T
 #define APE_LZ4_EAGER_T 16
 #endif
 constexpr uint32_t kEagerLen = APE_LZ4_EAGER_T;   // match bytes measured by C1 (T candidate)
-static_assert(kEagerLen == 16 || kEagerLen == 20, "C1 measures T to 16 or 20 bytes");
+static_assert(kEagerLen == 12 || kEagerLen == 16 || kEagerLen == 20, "C1 measures T to 12, 16 or 20 bytes");
 constexpr int kYW = (int)(kEagerLen + 4u) / 4;   // T-candidate dwords loaded: in[T-4, T+kEagerLen)
 constexpr uint32_t kEagerL = 12;     // ... for the in-chunk candidate L
 // Stage 2 (C2) measures only the candidates C1 left truncated (~13 % of the lanes on App.
@@ -88,6 +101,15 @@ constexpr bool kWin = kRingE >= 65536u;
 #endif
 constexpr uint32_t kScr = 1u << APE_LZ4_SCRBITS;  // in-chunk candidate scratch entries
 constexpr int kSmall = 128;          // smaller blocks take the byte-load path
+// Sequence records in flight between the walker and the emitter: the emitter takes 64 at
+// a time, fewer than 64 + 16 (a chunk has <= 16 matches) are ever queued, so a batch
+// being read and the walker's next records never share a slot.
+constexpr uint32_t kQ = 128;
+#ifndef APE_EMIT_EVERY
+#define APE_EMIT_EVERY 8             // emitter: a batch every this many steps (at most)
+#endif
+constexpr uint32_t kStage = 512;     // emitter: output bytes per batch
+constexpr uint32_t kStageAlloc = kStage + 16u + 16u + 64u;   // + alignment, slack, dummies
 
 
 // info.x: len (7) | trunc << 7 | back << 8 (3) | hashable << 13;   info.y: offset | h << 16
@@ -101,12 +123,12 @@ struct __attribute__((aligned(16))) EncLds {
     // input byte x at ring byte (x mod kRingE); the first 64 bytes are mirrored
     // after the end, so a 36-byte read never wraps (immediate LDS offsets)
     uint32_t ring[kRingE / 4 + 16];
-    uint2 info[3][64];               // producer -> walker and emitter, chunk k in [k % 3]
+    uint2 info[2][64];               // producer -> walker, chunk k in [k & 1]
     uint32_t scr[kScr];              // producer scratch: earliest lane per low hash bits
-    uint2 wres[2][64];               // walker -> emitter: {m_len | m_back << 20, anchor}
-    uint32_t wmem[2][2];             // walker -> emitter: member mask of the chunk
-    uint32_t wend;                   // walker -> emitter: final anchor (last literals)
-    uint32_t omap[16];               // emitter: owner map of a 64-byte output window
+    uint2 q[kQ];                     // walker -> emitter: sequence records, record r in
+                                     // [r % kQ]: {lit | (match length - 4) << 16, offset}
+    uint32_t qn;                     // walker -> emitter: records published
+    uint8_t __attribute__((aligned(16))) stage[kStageAlloc];   // emitter: one batch's bytes
 };
 
 // s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt at their maxima = no wait).  The
@@ -118,6 +140,32 @@ __device__ __forceinline__ void vm_wait() {
     static_assert(N >= 0 && N < 16, "vmcnt");
     __builtin_amdgcn_s_waitcnt(N | (7 << 4) | (15 << 8));
 }
+
+// Diagnostic (sensitivity A/B only, never the product): N dependent-free 4-cycle VALU ops
+// (APE_EXP_PAD_P / _W / _PL: producer, walker VALU; producer LDS reads).
+template <int N>
+__device__ __forceinline__ void pad_valu(uint32_t &x) {
+#pragma unroll
+    for (int i = 0; i < N; i++) asm volatile("v_mul_u32_u24 %0, %0, 3" : "+v"(x));
+}
+template <int N>
+__device__ __forceinline__ void pad_lds(uint32_t &x) {
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        uint32_t y;
+        asm volatile("ds_read_b32 %0, %1 offset:16384" : "=v"(y) : "v"(x & 0x3FCu));
+        asm volatile("s_waitcnt lgkmcnt(0)\n v_add_u32 %0, %0, %1" : "+v"(x) : "v"(y));
+    }
+}
+#ifndef APE_EXP_PAD_P
+#define APE_EXP_PAD_P 0
+#endif
+#ifndef APE_EXP_PAD_W
+#define APE_EXP_PAD_W 0
+#endif
+#ifndef APE_EXP_PAD_PL
+#define APE_EXP_PAD_PL 0
+#endif
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -205,7 +253,9 @@ __device__ __forceinline__ void load32(gcu8 *in, int n, int pos, uint32_t (&X)[8
 __device__ __forceinline__ uint32_t hash5(uint32_t x1, uint32_t b4) {
     const uint32_t lo = x1 & 0xFFFFFFu, hi = (x1 >> 24) | ((b4 & 0xFFu) << 8);
     // (__umul24 returns int: do the sum and the shift unsigned)
-    return ((uint32_t)__umul24(lo, 0x9E3779u) + (uint32_t)__umul24(hi, 0xC2B2AEu)) >> (32 - kHLog);
+    const uint32_t v = (uint32_t)__umul24(lo, 0x9E3779u) + (uint32_t)__umul24(hi, 0xC2B2AEu);
+    if constexpr (kHSize == (1 << kHLog)) return v >> (32 - kHLog);
+    else return (uint32_t)__umul24(v >> 16, (uint32_t)kHSize) >> 16;
 }
 
 // v_ffbl_b32 / v_ffbh_u32: lowest / highest set bit, 0xFFFFFFFF for 0 (inline asm
@@ -585,7 +635,7 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
             trunc = mine == kExt2 && R.lim > R.base + kExt2;
         }
     }
-    S.info[k % 3][lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
+    S.info[k & 1][lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
                                          (R.hashable ? I_HASHABLE : 0u),
                                      (R.has ? p - R.c : 0u) | (R.h << 16));
 }
@@ -660,7 +710,7 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     const uint32_t P = 64u * (uint32_t)k;
     O.walked = O.members = 0;
     O.m_back = O.m_len = O.an = 0;
-    O.iv = S.info[k % 3][lane];
+    O.iv = S.info[k & 1][lane];
     O.q0 = W.q;
     O.Lf = O.iv.x & 0x7Fu;                               // forward match length
     if (W.q >= P + 64u) return;               // a match from earlier chunks covers it
@@ -734,7 +784,7 @@ __device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk 
 }
 
 __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int lane,
-                                             const WalkOut &O) {
+                                             const WalkOut &O, uint32_t &qn) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const uint2 iv = O.iv;
     if (lane_in(O.walked) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
@@ -763,134 +813,201 @@ __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int
     // land before these (compiler barrier only)
     __builtin_amdgcn_sched_barrier(0);
     if (e2ok) S.tab[e2h] = (uint16_t)e2;
-    S.wres[k & 1][lane] = make_uint2(O.m_len | (O.m_back << 20), O.an);
-    if (lane == 0) {
-        S.wmem[k & 1][0] = (uint32_t)O.members;
-        S.wmem[k & 1][1] = (uint32_t)(O.members >> 32);
-    }
+    // the chunk's sequences, in order, as records for the emitter: literals from the
+    // anchor to the match start (after catch-up), the match length and its offset
+    if (mem) S.q[(qn + lane_rank(O.members)) & (kQ - 1u)] =
+        make_uint2(((p - O.m_back) - O.an) | ((O.m_len - kMinMatch) << 16), iv.y & 0xFFFFu);
+    qn += (uint32_t)__popcll(O.members);
+    if (lane == 0) S.qn = qn;
 }
 
 // ---------------- emitter ----------------
-// Chunks are emitted in pairs (one 64-byte output window holds ~40 bytes of two
-// chunks' sequences instead of ~20 of one): sizes of each chunk in the second half
-// of step k + 2, both chunks' bytes in the first half of step kA + 4 (kA = the pair's
-// first chunk).
-struct EmitC {          // one chunk's sequences, per member lane
-    uint64_t members;
-    uint32_t tot, ex, an, lit, mo;
-};
+// Sequences are written one per lane from the walker's records, a batch at a time (every
+// 4 steps, ~18 records on App. C data):
+//   F (first half of a step): read the records, size them, prefix-sum output offsets and
+//     input positions, take the leading records whose output fits the 512-byte staging
+//     buffer, check the capacity, and write their bytes into the staging buffer -- token,
+//     length extensions, offset, and the literals copied from the input ring (the ring
+//     holds the last 13-16 chunks, and a batch's records are at most ~6 chunks old);
+//   C (second half): the staged bytes -> dst with one 16-byte store per lane.
+// No global memory is read, and one store instruction per batch is written: emitter
+// memory instructions stall the whole block (byte stores to scattered addresses, or a
+// literal re-read from global memory, measured +8-30 % encode time).  The staging buffer
+// keeps dst's 16-byte alignment (batch byte 0 at stage[o0 % 16]); only whole 16-byte
+// chunks go out, the last partial chunk stays and becomes the next batch's chunk 0.  A
+// "big" record -- literals no longer in the ring, or a record larger than the buffer
+// (long literal runs, in practice) -- is written straight to dst by the whole wave after
+// the copy.
 struct Emit {
     uint32_t o;          // output cursor
+    uint32_t ein;        // input position of the next record's literals (its anchor)
+    uint32_t qc;         // records consumed
+    int last;            // step of the last batch
     bool overflow;
-    bool pend;           // A (and B) prepared, not yet written
-    int kA;              // first chunk of the pending pair
-    EmitC A, Bc;
+    bool part;           // stage[0, o % 16) does not hold dst's bytes there
+    int pend;            // the pending batch's next piece: 0 none, 1 L, 2 H, 3 C
+    bool nv;             // per lane: a staged (not big) record
+    uint32_t o0, tot;    // output offset and bytes of the pending batch
+    uint64_t bigm;       // its big records, and per lane their token's staging index,
+    uint32_t r, lit, mlm4, off, ba;   // literal count, match length - 4, offset, literals
 };
 
-// Sizes and output offsets of chunk k's sequences into C; `before` = output bytes of
-// the pair's earlier chunk.
-__device__ __forceinline__ void emit_prepare(const EncLds &S, const Blk &B, int k, int lane, Emit &E,
-                                             EmitC &C, uint32_t before) {
-    C.tot = 0;
-    const uint64_t members = ((uint64_t)__builtin_amdgcn_readfirstlane(S.wmem[k & 1][1]) << 32) |
-                             (uint32_t)__builtin_amdgcn_readfirstlane(S.wmem[k & 1][0]);
-    C.members = E.overflow ? 0ull : members;
-    if (!C.members) return;
-    const uint2 wr = S.wres[k & 1][lane];
-    const uint32_t off = S.info[k % 3][lane].y & 0xFFFFu;
-    const bool mem = lane_in(C.members);
-    const uint32_t m_len = wr.x & 0xFFFFFu, m_back = wr.x >> 20;
-    const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-    const uint32_t ms = p - m_back;            // match start after catch-up
-    C.an = wr.y;
-    C.lit = mem ? ms - C.an : 0u;
-    const uint32_t ml = m_len - kMinMatch;
-    const uint32_t size = mem ? 1u + ext_bytes(C.lit) + C.lit + 2u + ext_bytes(ml) : 0u;
-    C.ex = wave_excl_scan(size);
-    C.tot = lane_val(C.ex + size, 63);
-    C.mo = ml | (off << 16);
-    // (32-bit: o <= cap < 2^31 and a chunk's output < 2^21, so the sum cannot wrap; a
-    // 64-bit compare of these uniform values went to the vector unit)
-    if (E.o + before + C.tot > B.cap) {
+// one staging byte per lane, branch-free: lanes with nothing to write hit their own dummy
+// byte past the buffer
+__device__ __forceinline__ void stage_put(EncLds &S, int lane, bool w, uint32_t at, uint32_t b) {
+    S.stage[w ? at : kStageAlloc - 64u + (uint32_t)lane] = (uint8_t)b;
+}
+
+// F: up to min(avail, 64) records from E.qc: sizes, offsets, capacity; input positions
+// below `rlo` will no longer be in the ring when the literals are copied (piece L).
+__device__ __forceinline__ void emit_fetch(EncLds &S, const Blk &B, int lane, Emit &E,
+                                           uint32_t avail, uint32_t rlo) {
+    const bool v0 = (uint32_t)lane < avail;
+    const uint2 rec = S.q[(E.qc + (uint32_t)lane) & (kQ - 1u)];
+    const uint32_t lit = v0 ? (rec.x & 0xFFFFu) : 0u, mlm4 = v0 ? (rec.x >> 16) : 0u;
+    const uint32_t size = v0 ? 3u + ext_bytes(lit) + lit + ext_bytes(mlm4) : 0u;
+    const uint32_t isz = wave_incl_sum(size);
+    // the leading records that fit the staging buffer (at least one)
+    const uint32_t nrec = umax((uint32_t)__popcll(wave_ballot(v0 && isz <= kStage)), 1u);
+    const bool v = (uint32_t)lane < nrec;
+    const uint32_t adv = v ? lit + mlm4 + kMinMatch : 0u;
+    const uint32_t iadv = wave_incl_sum(adv);
+    const uint32_t tot = lane_val(isz, (int)nrec - 1), tadv = lane_val(iadv, (int)nrec - 1);
+    E.qc += nrec;
+    if (E.overflow) return;
+    // (32-bit: o <= cap < 2^31 and a batch's output < 2^21)
+    if (E.o + tot > B.cap) {
         E.overflow = true;
-        C.members = 0;
-        C.tot = 0;
+        return;
+    }
+    E.ba = E.ein + (iadv - adv);                 // literal source
+    E.r = (E.o & 15u) + (isz - size);            // token's staging index
+    E.lit = v ? lit : 0u;
+    E.mlm4 = mlm4;
+    E.off = rec.y;
+    const bool big = v && (E.ba < rlo || size > kStage);
+    E.bigm = wave_ballot(big);
+    E.nv = v && !big;
+    E.o0 = E.o;
+    E.tot = tot;
+    E.o += tot;
+    E.ein += tadv;
+    E.pend = 1;
+}
+
+// L: the literals, from the input ring -> staging, 16 bytes per lane per trip (aligned
+// ring dwords + v_alignbyte: one LDS round trip), written as unaligned dwords.  A lane's
+// last dword may run up to 3 bytes past its literals: onto its own offset and the byte
+// after it (a match-length extension or the next record's token) -- header bytes, which
+// piece H writes afterwards.  (No other lane's literals start before those 3 bytes end.)
+__device__ __forceinline__ void emit_lits(EncLds &S, int lane, Emit &E) {
+    const bool nv = E.nv;
+    const uint32_t lit = E.lit, a = E.ba;
+    const uint32_t lo = E.r + 1u + ext_bytes(lit);
+    typedef uint32_t u32a __attribute__((aligned(1)));
+    for (uint32_t t = 0; wave_any(nv && t < lit); t += 16u) {
+        const uint4 w = ring16(S, a + t);
+        const uint32_t W[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (uint32_t u = 0; u < 4u; u++) {
+            const bool wr = nv && t + 4u * u < lit;
+            *(u32a *)(S.stage + (wr ? lo + t + 4u * u : kStageAlloc - 64u + 4u * ((uint32_t)lane & 15u))) = W[u];
+        }
+    }
+    E.pend = 2;
+}
+
+// H: token, literal-length extension, offset, match-length extension -> staging
+__device__ __forceinline__ void emit_heads(EncLds &S, int lane, Emit &E) {
+    const bool nv = E.nv;
+    const uint32_t lit = E.lit, mlm4 = E.mlm4, r = E.r;
+    const uint32_t elit = ext_bytes(lit), eml = ext_bytes(mlm4);
+    stage_put(S, lane, nv, r, (umin(lit, 15u) << 4) | umin(mlm4, 15u));
+    for (uint32_t k = 0; wave_any(nv && k < elit); k++)
+        stage_put(S, lane, nv && k < elit, r + 1u + k, umin(lit - 15u - mul255(k), 255u));
+    const uint32_t oo = r + 1u + elit + lit;
+    stage_put(S, lane, nv, oo, E.off);
+    stage_put(S, lane, nv, oo + 1u, E.off >> 8);
+    for (uint32_t k = 0; wave_any(nv && k < eml); k++)
+        stage_put(S, lane, nv && k < eml, oo + 2u + k, umin(mlm4 - 15u - mul255(k), 255u));
+    E.pend = 3;
+}
+
+// one sequence written straight to dst by the whole wave (big records)
+__device__ __forceinline__ void emit_one(const Blk &B, int lane, uint32_t o, uint32_t a,
+                                         uint32_t lit, uint32_t mlm4, uint32_t off) {
+    gu8 *dst = B.dst;
+    const uint32_t elit = ext_bytes(lit), eml = ext_bytes(mlm4);
+    const uint32_t oo = o + 1u + elit + lit;
+    if (lane == 0) dst[o] = (uint8_t)((umin(lit, 15u) << 4) | umin(mlm4, 15u));
+    for (uint32_t k = (uint32_t)lane; k < elit; k += 64u)
+        dst[o + 1u + k] = (uint8_t)umin(lit - 15u - 255u * k, 255u);
+    wave_copy(B.in, dst, a, o + 1u + elit, lit, lane);
+    if (lane < 2) dst[oo + (uint32_t)lane] = (uint8_t)(off >> (8 * lane));
+    for (uint32_t k = (uint32_t)lane; k < eml; k += 64u)
+        dst[oo + 2u + k] = (uint8_t)umin(mlm4 - 15u - 255u * k, 255u);
+}
+
+// C: the staged batch -> dst.  stage[16 c, 16 c + 16) holds dst[a + 16 c, a + 16 c + 16),
+// a = o0 rounded down to 16; the batch covers stage[s0, s0 + tot), s0 = o0 % 16.  Only
+// whole chunks go out; the last partial chunk moves to stage[0, 16).  After a batch with a
+// big record everything goes out, the partial chunk by byte stores, and the next batch's
+// chunk 0 then holds only its own bytes (E.part).
+__device__ __forceinline__ void emit_copy(EncLds &S, const Blk &B, int lane, Emit &E) {
+    E.pend = 0;
+    const uint32_t s0 = E.o0 & 15u, end = s0 + E.tot;
+    gu8 *out = B.dst + (E.o0 - s0);
+    const uint32_t c0 = 16u * (uint32_t)lane;
+    const uint64_t bigm = E.bigm;
+    const uint32_t nfull = end >> 4;   // (a batch with one big record can pass kStage:
+                                       // only its staged chunks, the rest is direct)
+    const bool head = E.part && s0 != 0u;   // chunk 0 is partial: dst holds its start
+    if ((uint32_t)lane < umin(nfull, kStage / 16u + 1u) && !(head && lane == 0))
+        gstore16(out + c0, *(const uint4 *)(S.stage + c0));
+    if (head || (bigm && (end & 15u) && nfull <= kStage / 16u)) {   // rare: byte stores
+        const uint32_t pc = (head && lane == 0) ? 0u : 16u * nfull;
+        const bool act = (head && lane == 0) || (bigm && (end & 15u) && lane == 1);
+        const uint4 w = *(const uint4 *)(S.stage + (act ? pc : 0u));
+        const uint32_t W[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (uint32_t t = 0; t < 16u; t++)
+            if (act && pc + t >= s0 && pc + t < end) out[pc + t] = (uint8_t)(W[t >> 2] >> (8 * (t & 3)));
+    }
+    if (bigm) {
+        vm_wait<0>();   // the copy above first: a big record's bytes overwrite it
+        for (uint64_t m = bigm; m; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            emit_one(B, lane, E.o0 - s0 + lane_val(E.r, j), lane_val(E.ba, j), lane_val(E.lit, j),
+                     lane_val(E.mlm4, j), lane_val(E.off, j));
+        }
+        E.part = true;
+    } else {
+        if (lane == 0) {   // carry the partial chunk to stage[0, 16)
+            const uint4 t = *(const uint4 *)(S.stage + 16u * nfull);
+            *(uint4 *)S.stage = t;
+        }
+        // (a partial chunk 0 that is still partial keeps its bytes in dst only)
+        E.part = head && nfull == 0u;
     }
 }
 
-// Gather the pair (kA, kA + 1).  Lane L of window w produces output byte w + L; its
-// sequence is the last member starting at or before it (owner map + prefix max over
-// owners 1..64 = chunk A's lanes, 65..128 = chunk B's, B's all after A's), whose
-// record comes over by ds_bpermute.  One wave's LDS operations complete in order, so
-// the owner-map writes, the read-back and the clearing need no waits.
-__device__ __forceinline__ void emit_write(EncLds &S, const Blk &B, int kA, int lane, Emit &E) {
-    const uint32_t totA = E.A.tot, tot = totA + E.Bc.tot;
-    if (tot == 0) return;
-    const uint32_t P = 64u * (uint32_t)kA;
-    // runs in the first half of step kA + 4, while the producer copies chunk kA + 6
-    // into the ring (or after the last step): input [rlo, P + 384) is intact there
-    const uint32_t rlo = P + 448u > kRingE ? P + 448u - kRingE : 0u;
-    const bool memA = lane_in(E.A.members), memB = lane_in(E.Bc.members);
-    const uint32_t exA = E.A.ex, exB = totA + E.Bc.ex;
-    // member starts, ~0 for other lanes: the window tests below are single compares
-    const uint32_t sA = memA ? exA : 0xFFFFFFFFu, sB = memB ? exB : 0xFFFFFFFFu;
-    gu8 *out = B.dst + E.o;
-    for (uint32_t w = 0; w < tot; w += 64u) {
-        const bool markA = sA - w - 1u < 63u;    // w < start < w + 64
-        const bool markB = sB - w - 1u < 63u;
-        if (markA) ((uint8_t *)S.omap)[exA - w] = (uint8_t)(lane + 1);
-        if (markB) ((uint8_t *)S.omap)[exB - w] = (uint8_t)(lane + 65);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t mk = ((const uint8_t *)S.omap)[lane];
-        __builtin_amdgcn_sched_barrier(0);
-        if (markA) ((uint8_t *)S.omap)[exA - w] = 0;
-        if (markB) ((uint8_t *)S.omap)[exB - w] = 0;
-        const uint64_t covA = wave_ballot(sA <= w);   // member 0 of A starts at 0
-        const uint64_t covB = wave_ballot(sB <= w);
-        const uint32_t carry = covB ? 128u - (uint32_t)__clzll((long long)covB)
-                                    : 64u - (uint32_t)__clzll((long long)covA);
-        const uint32_t own = umax(wave_incl_max(mk), carry) - 1u;
-        const int sl = (int)((own & 63u) << 2);
-        const bool fb = own >= 64u;
-        // all eight permutes by every lane (a permute reads its source lane's register,
-        // so it must not run under a lane-dependent condition), then a select
-        const uint32_t a_ex = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)exA);
-        const uint32_t b_ex = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)exB);
-        const uint32_t a_an = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.an);
-        const uint32_t b_an = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.an);
-        const uint32_t a_li = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.lit);
-        const uint32_t b_li = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.lit);
-        const uint32_t a_mo = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.A.mo);
-        const uint32_t b_mo = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)E.Bc.mo);
-        const uint32_t r_ex = fb ? b_ex : a_ex, r_an = fb ? b_an : a_an;
-        const uint32_t rl = fb ? b_li : a_li, r_mo = fb ? b_mo : a_mo;
-        const uint32_t b = w + (uint32_t)lane;
-        // every candidate value computed, then selected (no divergent branches)
-        const uint32_t rr = b - r_ex;                    // offset inside the sequence
-        const uint32_t rml = r_mo & 0xFFFFu, roff = r_mo >> 16;
-        const uint32_t lit_at = 1u + ext_bytes(rl), off_at = lit_at + rl;
-        const uint32_t a = r_an + (rr - lit_at);         // literal source position
-        uint32_t v = ((const uint8_t *)S.ring)[a & (kRingE - 1)];
-        // a literal older than the ring (rare) comes from the input.  The load sits in a
-        // wave-uniform branch with its own wait: as a plain conditional load, the compiler's
-        // wait before the merged value was an s_waitcnt vmcnt(0) on every window, which (vmcnt
-        // counts stores too) drained the previous windows' output stores each time.
-        const bool older = rr >= lit_at && rr < off_at && a < rlo;
-        if (wave_any(older)) {
-            if (older) v = B.in[a];
-            vm_wait<0>();
-        }
-        // length extension bytes: 255 while more than 254 remain, then the rest
-        // (the i-th byte after the nibble is min(255, v - 15 - 255 i))
-        const uint32_t vl = umin(rl - 15u - mul255(rr - 1u), 255u);
-        const uint32_t vm = umin(rml - 15u - mul255(rr - off_at - 2u), 255u);
-        const uint32_t vo = rr == off_at ? (roff & 0xFFu) : (roff >> 8);
-        v = rr < off_at ? v : (rr < off_at + 2u ? vo : vm);
-        v = rr < lit_at ? vl : v;
-        v = rr == 0u ? ((umin(rl, 15u) << 4) | umin(rml, 15u)) : v;
-        if (b < tot) out[b] = (uint8_t)v;
-    }
-    E.o += tot;
+// the pending batch's next piece (or all of them)
+__device__ __forceinline__ void emit_step(EncLds &S, const Blk &B, int lane, Emit &E) {
+    if (E.pend == 1) emit_lits(S, lane, E);
+    else if (E.pend == 2) emit_heads(S, lane, E);
+    else if (E.pend == 3) emit_copy(S, B, lane, E);
+}
+__device__ __forceinline__ void emit_all(EncLds &S, const Blk &B, int lane, Emit &E) {
+    if (E.pend == 1) emit_lits(S, lane, E);
+    if (E.pend == 2) emit_heads(S, lane, E);
+    if (E.pend == 3) emit_copy(S, B, lane, E);
+}
+
+// the carried partial chunk (output bytes [o rounded down to 16, o)) -> dst
+__device__ __forceinline__ void emit_tail(EncLds &S, const Blk &B, int lane, Emit &E) {
+    const uint32_t s0 = E.o & 15u;
+    if (!E.part && s0 != 0u && (uint32_t)lane < s0)
+        B.dst[E.o - s0 + (uint32_t)lane] = S.stage[lane];
 }
 
 // ---------------- history prefix (withPrefix encode) ----------------
@@ -961,6 +1078,8 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             vm_wait<kWin ? 1 : 4>();
             STAT(9);
             prod_measure<SMALL, F>(S, B, s + 1, lane, X6, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q);
+            if (APE_EXP_PAD_P) { uint32_t x = (uint32_t)lane; pad_valu<APE_EXP_PAD_P>(x); (void)x; }
+            if (APE_EXP_PAD_PL) { uint32_t x = (uint32_t)lane; pad_lds<APE_EXP_PAD_PL>(x); (void)x; }
             STAT(5);
             __syncthreads();
             STAT(6);
@@ -1014,6 +1133,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
     }
     if (wave == 0) {   // walker: chunk s-1 during step s
         Walk W;
+        uint32_t qn = 0;
         W.q = 64u * (uint32_t)k0;
         W.anchor = W.q;
         W.dense = 3u;   // the first search probes 0, 1, 2, then every stride-th
@@ -1026,15 +1146,15 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             const bool work = s >= k0 + 1 && s <= nch;
 #endif
             if (work) walk_chain<ACC>(S, B, s - 1, lane, W, O);
+            if (APE_EXP_PAD_W) { uint32_t x = (uint32_t)lane; pad_valu<APE_EXP_PAD_W>(x); (void)x; }
             STAT(0);
             __syncthreads();
             STAT(4);
             if (work) {
                 walk_finish<ACC>(B, s - 1, lane, W, O);
-                walk_publish(S, B, s - 1, lane, O);
+                walk_publish(S, B, s - 1, lane, O, qn);
                 STAT_ADD(11, __popcll(O.members));
             }
-            if (s == nsteps - 1 && lane == 0) S.wend = W.anchor;
             STAT(1);
             STAT_ADD(10, 3);
             __syncthreads();
@@ -1043,65 +1163,60 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         STATS_FLUSH(g_enc_stats);
         return;
     }
-    // emitter: sizes of chunk s-2 in the second half of step s (the walker published it
-    // in step s-1); the bytes of a pair (kA, kA+1) in the first half of step kA+4 --
-    // next to the producer's and the walker's long first halves
+    // emitter: a batch every 4 steps (F in a first half, C in the second half); a queue of
+    // 48+ records (never on App. C data) starts one at once; the rest after the last step
     Emit E;
     E.o = 0;
+    E.ein = 64u * (uint32_t)k0;
+    E.qc = 0;
+    E.last = k0;
     E.overflow = false;
-    E.pend = false;
-    E.kA = k0;
-    E.A.members = E.Bc.members = 0;
-    E.A.tot = E.A.ex = E.A.an = E.A.lit = E.A.mo = 0;
-    E.Bc.tot = E.Bc.ex = E.Bc.an = E.Bc.lit = E.Bc.mo = 0;
+    E.part = false;
+    E.pend = 0;
+    E.nv = false;
+    E.o0 = E.tot = 0;
+    E.bigm = 0;
+    E.r = E.lit = E.mlm4 = E.off = E.ba = 0;
     __syncthreads();
     for (int s = k0; s < nsteps; s++) {
-#ifdef APE_EXP_NOEMIT
-        const bool work = false;   // diagnostic: instruction count without the emitter
-#else
-        const bool work = true;
-#endif
-        const int r = s - k0;
-#ifdef APE_EMIT_SINGLE
-        if (work && E.pend && E.kA == s - 3) {   // diagnostic: one chunk per write
-            emit_write(S, B, s - 3, lane, E);
-            E.pend = false;
+        // S.qn: the walker's count as of its last publish (before the previous barrier)
+        const uint32_t avail = (uint32_t)__builtin_amdgcn_readfirstlane(S.qn) - E.qc;
+        if (E.pend == 0) {
+            if (avail != 0u && (avail >= 48u || s - E.last >= APE_EMIT_EVERY)) {
+                // piece L runs in the second half of step s, when the ring holds input
+                // [64 (s - 12), 64 (s + 4)) (chunk s + 3 is being written over s - 13)
+                emit_fetch(S, B, lane, E, avail, s >= 12 ? 64u * (uint32_t)(s - 12) : 0u);
+                E.last = s;
+            }
+        } else if (avail >= 80u) {   // rare: never on App. C data
+            emit_all(S, B, lane, E);
+        } else {
+            emit_step(S, B, lane, E);
         }
-#else
-        if (work && E.pend && E.kA == s - 4) {   // the pair prepared in steps s-2, s-1
-#ifndef APE_EXP_NOWRITE   // diagnostic: instruction count without the output windows
-            emit_write(S, B, s - 4, lane, E);
-#endif
-            E.pend = false;
-        }
-#endif
         STAT(2);
         __syncthreads();
         STAT(14);
-        if (work && r >= 2 && s - 2 < nch) {
-#ifdef APE_EMIT_SINGLE
-            if (true) {
-#else
-            if (((r - 2) & 1) == 0) {            // first chunk of a pair
-#endif
-                E.Bc.members = 0;
-                E.Bc.tot = 0;
-                emit_prepare(S, B, s - 2, lane, E, E.A, 0u);
-                E.kA = s - 2;
-                E.pend = true;
-            } else {
-                emit_prepare(S, B, s - 2, lane, E, E.Bc, E.A.tot);
-            }
-        }
+        if (E.pend == 1 || E.pend == 3) emit_step(S, B, lane, E);   // L or C
         STAT(12);
         __syncthreads();
         STAT(15);
     }
-    // the last pair may still be pending (its write step lies past the loop)
-    if (E.pend) emit_write(S, B, E.kA, lane, E);
-    // ---- last literals (:732-751), from the walker's final anchor ----
+    // every record is published now (the walker's last publish preceded the last barrier);
+    // the ring holds the last 16 chunks
+    emit_all(S, B, lane, E);
+    {
+        const uint32_t rlo = B.nch > 16 ? 64u * (uint32_t)(B.nch - 16) : 0u;
+        for (uint32_t left = (uint32_t)__builtin_amdgcn_readfirstlane(S.qn) - E.qc; left;) {
+            const uint32_t qc0 = E.qc;
+            emit_fetch(S, B, lane, E, left, rlo);
+            emit_all(S, B, lane, E);
+            left -= E.qc - qc0;
+        }
+    }
+    if (!E.overflow) emit_tail(S, B, lane, E);
+    // ---- last literals (:732-751), from the end of the last match ----
     if (!E.overflow) {
-        const uint32_t anchor = S.wend;
+        const uint32_t anchor = E.ein;
         const uint32_t lit = B.un - anchor;
         const uint32_t hdr = 1u + ext_bytes(lit);
         const uint32_t total = E.o + hdr + lit;
@@ -1126,7 +1241,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
 // ACC: compress_fast with acceleration > 1 (its own instantiation, so the default
 // kernel carries none of the probe-pattern code)
 template <bool ACC>
-__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(6)))
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(APE_LZ4_WAVES_PER_EU)))
 lz4_encode_kernel(BlockArgs a) {
     __shared__ EncLds S;
     const int b = blockIdx.x;
@@ -1173,7 +1288,7 @@ lz4_encode_kernel(BlockArgs a) {
     for (int i = tid; i < kHSize / 8; i += 192) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
     for (int i = tid; i < (int)kScr; i += 192) S.scr[i] = 0xFFFFFFFFu;
     for (int i = tid; i < (int)(kRingE / 16 + 4); i += 192) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
-    if (tid < 16) S.omap[tid] = 0u;
+    if (tid == 0) S.qn = 0u;
     __syncthreads();
     if (B.n < kSmall) encode_block<true, ACC>(S, B, wave, lane, &a.result[b]);
     else encode_block<false, ACC>(S, B, wave, lane, &a.result[b]);

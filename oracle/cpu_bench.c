@@ -354,3 +354,267 @@ void cpu_bench_free(void *h)
     dlclose(b->dl);
     free(b);
 }
+
+/* ---------------------------------------------------------------------------------
+ * cpu_sock_run: the reference's own LZ4 socket codec over loopback TCP (BASELINE config
+ * 5 CPU baseline).  Restates the codec calls of ape_socket.c without
+ * its event loop:
+ *   TX (ape_socket_write, src/ape_socket.c:811-871): each message is cut into 8 KiB
+ *     blocks (APE_LZ4_BLOCK_SIZE, :39), each compressed with compress_fast_continue
+ *     (accel 1) into [int32 size][block], then saveDict(64 KiB) (:856); write() the frames;
+ *   RX (ape_socket_read_lz4_stream, :1333-1467): read() into a buffer, take complete
+ *     frames [int32 size][block] (a split-safe parser: the reference's desyncs),
+ *     decompress_safe_continue into an 8 KiB block, append it to the 64 KiB dictionary
+ *     buffer (memmove when full, :1398-1413) and setStreamDecode on it (:1421).
+ * One TX and one RX thread per connection; messages are the App. C blocks of
+ * `msg` bytes (the benchmark's 64 KiB).  out: [0] seconds, [1] payload bytes,
+ * [2] wire bytes, [3] errors.
+ * --------------------------------------------------------------------------------- */
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+typedef void *(*smk_fn)(void);
+typedef int (*sfree_fn)(void *);
+typedef int (*scc_fn)(void *, const char *, char *, int, int, int);
+typedef int (*ssave_fn)(void *, char *, int);
+typedef int (*sdc_fn)(void *, const char *, char *, int, int);
+typedef int (*ssetd_fn)(void *, const char *, int);
+
+enum { SK_BLOCK = 8192, SK_DICT = 65536 };
+
+typedef struct {
+    smk_fn mk, mkd;
+    sfree_fn fr, frd;
+    scc_fn cc;
+    ssave_fn save;
+    sdc_fn dc;
+    ssetd_fn setd;
+    int fd_tx, fd_rx, msg, nmsg, kind, conn;
+    long long wire;
+    int bad;
+} sconn_t;
+
+static int sk_write_all(int fd, const char *p, size_t n)
+{
+    while (n) {
+        ssize_t w = write(fd, p, n);
+        if (w <= 0) return -1;
+        p += w;
+        n -= (size_t)w;
+    }
+    return 0;
+}
+
+static void *sk_tx(void *arg)
+{
+    sconn_t *c = (sconn_t *)arg;
+    const int cap = SK_BLOCK + SK_BLOCK / 255 + 16;
+    uint8_t *msg = malloc((size_t)c->msg);
+    char *frames = malloc((size_t)(c->msg / SK_BLOCK + 1) * (cap + 4));
+    char *dict = malloc(SK_DICT);
+    void *st = c->mk();
+    for (int m = 0; m < c->nmsg && st; m++) {
+        synth_blocks(msg, c->msg, c->msg, (long long)c->conn * c->nmsg + m, 1, c->kind);
+        int pos = 0;
+        for (int off = 0; off < c->msg; off += SK_BLOCK) {
+            const int len = c->msg - off < SK_BLOCK ? c->msg - off : SK_BLOCK;
+            const int r = c->cc(st, (const char *)msg + off, frames + pos + 4, len, cap, 1);
+            if (r <= 0) { c->bad++; break; }
+            memcpy(frames + pos, &r, 4);
+            pos += 4 + r;
+        }
+        c->save(st, dict, SK_DICT);
+        if (sk_write_all(c->fd_tx, frames, (size_t)pos) != 0) { c->bad++; break; }
+        c->wire += pos;
+    }
+    shutdown(c->fd_tx, SHUT_WR);
+    if (st) c->fr(st);
+    free(msg); free(frames); free(dict);
+    return NULL;
+}
+
+static void *sk_rx(void *arg)
+{
+    sconn_t *c = (sconn_t *)arg;
+    const int cap = SK_BLOCK + SK_BLOCK / 255 + 16;
+    const size_t bsz = 1u << 20;
+    char *buf = malloc(bsz);
+    char *dict = malloc(SK_DICT);
+    char tmp[SK_BLOCK];
+    uint8_t *expect = malloc((size_t)c->msg);
+    void *sd = c->mkd();
+    size_t used = 0;
+    int dpos = 0, m = 0, mpos = 0;
+    synth_blocks(expect, c->msg, c->msg, (long long)c->conn * c->nmsg, 1, c->kind);
+    for (;;) {
+        ssize_t r = read(c->fd_rx, buf + used, bsz - used);
+        if (r < 0) { c->bad++; break; }
+        used += (size_t)r;
+        size_t p = 0;
+        while (used - p >= 4) {
+            int32_t sz;
+            memcpy(&sz, buf + p, 4);
+            if (sz <= 0 || sz > cap) { c->bad++; goto done; }
+            if (used - p - 4 < (size_t)sz) break;
+            const int rc = c->dc(sd, buf + p + 4, tmp, sz, SK_BLOCK);
+            if (rc <= 0) { c->bad++; goto done; }
+            if (dpos + rc > SK_DICT) {   /* :1398-1413 */
+                const int need = rc - (SK_DICT - dpos);
+                memmove(dict, dict + need, (size_t)(dpos - need));
+                memcpy(dict + dpos - need, tmp, (size_t)rc);
+                dpos = SK_DICT;
+            } else {
+                memcpy(dict + dpos, tmp, (size_t)rc);
+                dpos += rc;
+            }
+            c->setd(sd, dict, dpos);
+            if (m < c->nmsg && memcmp(tmp, expect + mpos, (size_t)rc) != 0) c->bad++;
+            mpos += rc;
+            if (mpos == c->msg && ++m < c->nmsg) {
+                mpos = 0;
+                synth_blocks(expect, c->msg, c->msg, (long long)c->conn * c->nmsg + m, 1, c->kind);
+            }
+            p += 4 + (size_t)sz;
+        }
+        memmove(buf, buf + p, used - p);
+        used -= p;
+        if (r == 0) break;
+    }
+done:
+    if (m != c->nmsg) c->bad++;
+    if (sd) c->frd(sd);
+    free(buf); free(dict); free(expect);
+    return NULL;
+}
+
+int cpu_sock_run(const char *lib, const char *prefix, int nconn, int msg, int nmsg, int kind,
+                 double *out)
+{
+    char name[128];
+    void *h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+    if (!h || nconn < 1 || nconn > 128 || msg <= 0 || nmsg < 0) return -1;
+    sconn_t base;
+    memset(&base, 0, sizeof base);
+#define SYM(var, type, nm) snprintf(name, sizeof name, "%s" nm, prefix); base.var = (type)dlsym(h, name)
+    SYM(mk, smk_fn, "createStream");
+    SYM(fr, sfree_fn, "freeStream");
+    SYM(mkd, smk_fn, "createStreamDecode");
+    SYM(frd, sfree_fn, "freeStreamDecode");
+    SYM(cc, scc_fn, "compress_fast_continue");
+    SYM(save, ssave_fn, "saveDict");
+    SYM(dc, sdc_fn, "decompress_safe_continue");
+    SYM(setd, ssetd_fn, "setStreamDecode");
+#undef SYM
+    if (!base.mk || !base.fr || !base.mkd || !base.frd || !base.cc || !base.save || !base.dc ||
+        !base.setd)
+        return -2;
+    sconn_t *cs = calloc((size_t)nconn, sizeof(sconn_t));
+    pthread_t *th = calloc((size_t)nconn * 2, sizeof(pthread_t));
+    int rc = 0;
+    for (int i = 0; i < nconn && rc == 0; i++) {
+        cs[i] = base;
+        cs[i].msg = msg; cs[i].nmsg = nmsg; cs[i].kind = kind; cs[i].conn = i;
+        int ls = socket(AF_INET, SOCK_STREAM, 0), one = 1;
+        struct sockaddr_in a;
+        socklen_t al = sizeof a;
+        memset(&a, 0, sizeof a);
+        a.sin_family = AF_INET;
+        a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+        setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+        if (ls < 0 || bind(ls, (struct sockaddr *)&a, sizeof a) || listen(ls, 1) ||
+            getsockname(ls, (struct sockaddr *)&a, &al)) { rc = -3; break; }
+        cs[i].fd_tx = socket(AF_INET, SOCK_STREAM, 0);
+        if (connect(cs[i].fd_tx, (struct sockaddr *)&a, sizeof a)) { rc = -3; break; }
+        cs[i].fd_rx = accept(ls, NULL, NULL);
+        close(ls);
+        if (cs[i].fd_rx < 0) { rc = -3; break; }
+        int b = 4 << 20;
+        setsockopt(cs[i].fd_tx, SOL_SOCKET, SO_SNDBUF, &b, sizeof b);
+        setsockopt(cs[i].fd_rx, SOL_SOCKET, SO_RCVBUF, &b, sizeof b);
+    }
+    const double t0 = now_s();
+    for (int i = 0; i < nconn && rc == 0; i++) {
+        pthread_create(&th[2 * i], NULL, sk_tx, &cs[i]);
+        pthread_create(&th[2 * i + 1], NULL, sk_rx, &cs[i]);
+    }
+    long long wire = 0;
+    int bad = 0;
+    for (int i = 0; i < nconn && rc == 0; i++) {
+        pthread_join(th[2 * i], NULL);
+        pthread_join(th[2 * i + 1], NULL);
+        wire += cs[i].wire;
+        bad += cs[i].bad;
+    }
+    const double t1 = now_s();
+    for (int i = 0; i < nconn; i++) {
+        if (cs[i].fd_tx > 0) close(cs[i].fd_tx);
+        if (cs[i].fd_rx > 0) close(cs[i].fd_rx);
+    }
+    free(cs); free(th);
+    if (rc) return rc;
+    out[0] = t1 - t0;
+    out[1] = (double)nconn * nmsg * msg;
+    out[2] = (double)wire;
+    out[3] = bad;
+    return 0;
+}
+
+/* sock_ceiling: plain bytes over one loopback TCP connection (no codec), `chunk`-byte
+ * write()s from one thread and read()s into a buffer in another -- the ceiling of the
+ * config 5 byte path.  out: [0] seconds, [1] bytes. */
+typedef struct { int fd; long long n; int chunk; } rawc_t;
+
+static void *raw_tx(void *arg)
+{
+    rawc_t *c = (rawc_t *)arg;
+    char *b = malloc((size_t)c->chunk);
+    memset(b, 0x5a, (size_t)c->chunk);
+    for (long long left = c->n; left > 0;) {
+        const int k = left < c->chunk ? (int)left : c->chunk;
+        if (sk_write_all(c->fd, b, (size_t)k)) break;
+        left -= k;
+    }
+    shutdown(c->fd, SHUT_WR);
+    free(b);
+    return NULL;
+}
+
+int sock_ceiling(long long nbytes, int chunk, double *out)
+{
+    int ls = socket(AF_INET, SOCK_STREAM, 0), one = 1, b = 4 << 20;
+    struct sockaddr_in a;
+    socklen_t al = sizeof a;
+    memset(&a, 0, sizeof a);
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    if (ls < 0 || bind(ls, (struct sockaddr *)&a, sizeof a) || listen(ls, 1) ||
+        getsockname(ls, (struct sockaddr *)&a, &al)) return -1;
+    rawc_t c = {socket(AF_INET, SOCK_STREAM, 0), nbytes, chunk};
+    if (connect(c.fd, (struct sockaddr *)&a, sizeof a)) return -1;
+    const int rfd = accept(ls, NULL, NULL);
+    close(ls);
+    setsockopt(c.fd, SOL_SOCKET, SO_SNDBUF, &b, sizeof b);
+    setsockopt(rfd, SOL_SOCKET, SO_RCVBUF, &b, sizeof b);
+    char *buf = malloc(1u << 20);
+    pthread_t th;
+    const double t0 = now_s();
+    pthread_create(&th, NULL, raw_tx, &c);
+    long long got = 0;
+    for (;;) {
+        ssize_t r = read(rfd, buf, 1u << 20);
+        if (r <= 0) break;
+        got += r;
+    }
+    pthread_join(th, NULL);
+    const double t1 = now_s();
+    close(c.fd);
+    close(rfd);
+    free(buf);
+    out[0] = t1 - t0;
+    out[1] = (double)got;
+    return got == nbytes ? 0 : -2;
+}

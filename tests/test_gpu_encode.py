@@ -318,3 +318,43 @@ def test_destSize_scratch_form_matches_and_captures(cuda, product, oracle):
         assert r > 0
         dr, out = orc_decompress(oracle, c, k)
         assert dr == k and out == s[:k]
+
+
+def _mixed_runs(n, seed):
+    """Blocks whose sequences mix every emitter path: short literal runs and matches (the
+    staged batch), literal runs longer than 16 bytes and match-length extensions of 3+
+    bytes (written straight to dst), in random order, so that batches start and end at
+    every alignment."""
+    rng = random.Random(seed)
+    out = bytearray(rng.randbytes(64))
+    while len(out) < n:
+        k = rng.random()
+        if k < 0.15:
+            out += rng.randbytes(rng.randrange(17, 300))           # long literal run
+        elif k < 0.2:
+            off = rng.randrange(1, min(len(out), 65535))
+            for _ in range(rng.randrange(530, 2000)):                # long match
+                out.append(out[-off])
+        elif k < 0.6:
+            out += rng.randbytes(rng.randrange(0, 16))
+            off = rng.randrange(1, min(len(out), 65535))
+            for _ in range(rng.randrange(4, 40)):
+                out.append(out[-off])
+        else:
+            out.append(rng.randrange(256))
+    return bytes(out[:n])
+
+
+def test_emitter_batches_mixed(cuda, product, oracle):
+    """The batched emitter (staging buffer carried across batches, big records written
+    straight to dst, the partial chunk after them) on mixed sequences, aligned and
+    misaligned dst, and caps at the exact size and one below."""
+    srcs = [_mixed_runs(n, s) for s, n in enumerate([65536] * 12 + [300, 1000, 4097, 20000, 65535])]
+    for mis in (None, [(7 * i) % 16 for i in range(len(srcs))]):
+        rs, comps = run_encode(cuda, product, srcs, out_mis=mis)
+        for s, r, c in zip(srcs, rs, comps):
+            assert 0 < r <= product.compressBound(len(s))
+            check_valid(oracle, s, c)
+        rs2, comps2 = run_encode(cuda, product, srcs, caps=rs, out_mis=mis)
+        assert rs2 == rs and comps2 == comps
+        assert run_encode(cuda, product, srcs, caps=[r - 1 for r in rs], out_mis=mis)[0] == [0] * len(srcs)

@@ -221,7 +221,15 @@ static long model3(const uint8_t *in, int n, int hlog, int R, int lag, int sb, i
  * same low `sb` hash bits; catch-up <= 4.  pol 0: T and L measured in full, longer
  * wins (tie: closer); pol 7: L measured to 12 bytes only, taken when T is shorter
  * than 12 and L at least as long (the product since the L-12 change). */
-static long model4(const uint8_t *in, int n, int lag, int pol, int sb)
+static int g_tsize = 8192;   /* model4 table entries (hash scaled onto [0, g_tsize)) */
+static uint32_t hslot(const uint8_t *p) {
+    if (g_tsize == 8192) return hsh(p, 13);
+    uint32_t x = rd32(p), b4 = p[4];
+    uint32_t lo = x & 0xFFFFFF, hi = (x >> 24) | (b4 << 8);
+    uint32_t v = lo * 0x9E3779u + hi * 0xC2B2AEu;
+    return (uint32_t)(((uint64_t)(v >> 16) * (uint32_t)g_tsize) >> 16);
+}
+static long model4(const uint8_t *in, int n, int lag, int pol, int sb, int lmax)
 {
     int tab[8192];
     for (int i = 0; i < 8192; i++) tab[i] = -1;
@@ -234,16 +242,16 @@ static long model4(const uint8_t *in, int n, int lag, int pol, int sb)
     for (int k = 0; k < nch; k++) {
         while (done < nins && insc[done] <= k - lag - 1) {
             int q = ins[done++];
-            if (q + 8 <= n) tab[hsh(in + q, 13)] = q;
+            if (q + 8 <= n) tab[hslot(in + q)] = q;
         }
         int r0 = 64 * k, r1 = r0 + 64 < n ? r0 + 64 : n;
         for (int i = 0; i < (1 << sb); i++) scr[i] = -1;
         for (int q = r0; q < r1; q++) {
-            uint32_t h = q + 8 <= n ? hsh(in + q, 13) : 0;
-            int s2 = h & ((1 << sb) - 1);
+            uint32_t h = q + 8 <= n ? hslot(in + q) : 0;
+            int s2 = (q + 8 <= n ? hsh(in + q, 13) : 0) & ((1 << sb) - 1);
             cT[q] = tab[h];
             cL[q] = -1;
-            if (scr[s2] < 0) scr[s2] = q; else cL[q] = scr[s2];
+            if (scr[s2] < 0) scr[s2] = q; else if (k < lmax) cL[q] = scr[s2];
         }
         while (p < r1) {
             int best = 0, bc = -1;
@@ -334,9 +342,30 @@ int main(int argc, char **argv)
     }
     for (int pol = 0; pol <= 7; pol += 7) {
         long tot = 0;
-        for (int b = 0; b < nb; b++) tot += model4(buf + (size_t)b * n, n, 3, pol, 6);
+        for (int b = 0; b < nb; b++) tot += model4(buf + (size_t)b * n, n, 3, pol, 6, 1 << 20);
         printf("kernel policy: lag 3, L bits 6, pol %d                  ratio %.4f\n", pol,
                (double)n * nb / tot);
+    }
+    {   /* the in-chunk candidate only for the first lmax chunks (short offsets cluster at
+           the block start: App. C offsets are uniform over the window so far) */
+        const int lm[] = {0, 2, 4, 8, 16, 32, 64, 128, 1 << 20};
+        for (unsigned k = 0; k < sizeof(lm) / sizeof(lm[0]); k++) {
+            long tot = 0;
+            for (int b = 0; b < nb; b++) tot += model4(buf + (size_t)b * n, n, 3, 7, 6, lm[k]);
+            printf("kernel policy pol 7, L for the first %7d chunks          ratio %.4f\n", lm[k],
+                   (double)n * nb / tot);
+        }
+    }
+    {
+        const int ts[] = {8192, 7552, 7168, 7040, 6656, 6144, 4096};
+        for (unsigned k = 0; k < sizeof(ts) / sizeof(ts[0]); k++) {
+            long tot = 0;
+            g_tsize = ts[k];
+            for (int b = 0; b < nb; b++) tot += model4(buf + (size_t)b * n, n, 3, 7, 6, 1 << 20);
+            printf("kernel policy pol 7, table of %5d entries                 ratio %.4f\n", ts[k],
+                   (double)n * nb / tot);
+        }
+        g_tsize = 8192;
     }
     free(buf);
     return 0;
