@@ -598,9 +598,22 @@ def sock_leg(args):
 
     run(min(nb, 2 * batch))                    # warm-up (kernels, allocations)
     h_dst.zero_()
+    amd.socket_stats(reset=True)
     wall, got, wire = run(nb)
+    split = amd.socket_stats(reset=True)
     ok = got == nb and bool((res == n).all()) and bool(torch.equal(h_dst, h_src))
-    return {
+    # the same wire bytes through the same kind of connection without the codec
+    ceiling = None
+    try:
+        cb = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
+        cb.sock_ceiling.argtypes = [C.c_longlong, C.c_int, C.POINTER(C.c_double)]
+        o2 = (C.c_double * 2)()
+        if cb.sock_ceiling(int(wire), 4 << 20, o2) == 0:
+            ceiling = round(o2[1] / o2[0] / 1e9, 3)
+    except OSError:
+        pass
+    cpu = None if args.no_cpu_baseline else cpu_sock_baseline(n)
+    line = {
         "metric": "LZ4 GiB/s through a loopback TCP socket (GPU encode -> frames -> socket -> "
                   "pinned rxbuf -> GPU decode), BASELINE config 5",
         "value": round(nb * n / wall / GIB, 3), "unit": "GiB/s", "n_gpus": 1,
@@ -610,8 +623,46 @@ def sock_leg(args):
                                "per GPU batch" % (nb, n >> 10, batch)},
         "wall_s": round(wall, 3), "wire_bytes": int(wire), "ratio": round(nb * n / (wire - 4 * nb), 4),
         "wire_GBps": round(wire / wall / 1e9, 3), "verified": ok,
-        "reference_loopback_GiBps": "0.25-0.33 (BASELINE.md config 5, reference CPU codec)",
+        "ceiling_GBps": ceiling,
+        "ceiling": "plain bytes over one 127.0.0.1 TCP connection, 4 MiB write()s, no codec "
+                   "(oracle/cpu_bench.c sock_ceiling), same wire bytes",
+        "split_ms": split,
+        "split_note": "GPU phases from timing events per batch (they overlap each other and "
+                      "the socket I/O: double-buffered); write/read = time in the syscalls; "
+                      "gpu_wait = host blocked on the GPU",
+        "cpu_baseline": cpu,
     }
+    line["bound"] = ("socket" if ceiling and line["wire_GBps"] >= 0.8 * ceiling else "pipeline")
+    return line
+
+
+def cpu_sock_baseline(n):
+    """The reference's own socket codec over loopback TCP on this host's cores (BASELINE
+    config 5; oracle/cpu_bench.c cpu_sock_run: ape_socket.c's TX -- 8 KiB blocks with
+    compress_fast_continue + saveDict -- and RX -- decompress_safe_continue against the 64 KiB
+    dictionary buffer -- without the event loop): one connection (a TX and an RX thread,
+    as one event loop would serve it) and usable/2 connections in parallel."""
+    lib = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
+    lib.cpu_sock_run.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.POINTER(C.c_double)]
+    ref = os.path.join(ROOT, "oracle", "_ref", "libape_lz4_ref.so")
+    if os.path.exists(ref):
+        path, prefix, kind = ref, b"APE_LZ4_", "reference"
+    else:
+        path, prefix, kind = os.path.join(ROOT, "oracle", "liblz4_oracle.so"), b"orc_", "port"
+    usable, cores = host_cores()
+    out = (C.c_double * 4)()
+    res = {}
+    for label, nconn, nmsg in (("one_connection", 1, 16384), ("all_cores", max(1, usable // 2), 4096)):
+        if lib.cpu_sock_run(path.encode(), prefix, nconn, n, nmsg, 1, out) != 0 or out[3] != 0:
+            return None
+        res[label] = {"value": round(out[1] / out[0] / GIB, 3), "connections": nconn,
+                      "wire_GBps": round(out[2] / out[0] / 1e9, 3), "seconds": round(out[0], 2)}
+    return {"value": res["one_connection"]["value"], "unit": "GiB/s", "cores": 2, "kind": kind,
+            "sample": "1 connection x %d x 64 KiB App. C messages (1 TX + 1 RX thread); also "
+                      "%d connections x 4096 messages on %d threads" % (
+                          16384, res["all_cores"]["connections"], 2 * res["all_cores"]["connections"]),
+            "host": cores, **res}
 
 
 def sock_bench(args):
@@ -783,7 +834,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--sock", action="store_true",
                     help="config 5: loopback TCP socket TX/RX through the GPU codec")
-    ap.add_argument("--sock-blocks", type=int, default=1 << 14)
+    ap.add_argument("--sock-blocks", type=int, default=1 << 17,
+                    help="config 5 sample (131072 x 64 KiB = 8 GiB)")
     ap.add_argument("--sock-batch", type=int, default=2048)
     args = ap.parse_args()
     if args.e2e:

@@ -222,6 +222,14 @@ long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_strid
 long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int block_size,
                                      int nblocks, int batch, int *h_result);
 
+/* Time split of the socket calls since the last reset, out[16] in ms: TX [0] H2D, [1] encode
+ * + frame offsets + pack (GPU), [2] D2H, [3] write(), [4] host waiting for the GPU, [5]
+ * batches (count), [6] the whole send call; RX [7] the whole receive loop, [8] read(), [9]
+ * frame parse + leftover copy, [10] H2D, [11] decode (GPU), [12] D2H, [13] host waiting for
+ * the GPU, [14] batches (count), [15] receive-buffer growth.  GPU phases are timing events
+ * around each batch's stages.  reset != 0 zeroes the counters. */
+int APE_LZ4_socket_stats(double *out16, int reset);
+
 /* ---- synthetic benchmark data, device-side ----
  * kind 0 = random bytes, 1 = compressible; block b is seeded with first_block+b. */
 int APE_LZ4_synth_blocks_dev(char *d_out, size_t stride, int blockSize,

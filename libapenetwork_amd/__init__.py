@@ -21,7 +21,8 @@ __all__ = [
     "compress_prefix_batch", "decompress_dict_batch", "compress_fast_ptr_batch",
     "decompress_fast_ptr_batch", "compress_destSize_ptr_batch", "RxBuf",
     "compress_destSize_scratch_ptr_batch", "destSize_scratch_size",
-    "socket_send_blocks", "socket_recv_blocks", "set_oneshot_host_below", "oneshot_on_gpu",
+    "socket_send_blocks", "socket_recv_blocks", "socket_stats", "set_oneshot_host_below",
+    "oneshot_on_gpu",
     "ONESHOT_HOST_ALL",
 ]
 
@@ -89,6 +90,7 @@ def lib():
             "APE_LZ4_rxbuf_free": (None, [p]),
             "APE_LZ4_socket_send_blocks": (ll, [i, p, sz, i, i, i]),
             "APE_LZ4_socket_recv_blocks": (ll, [i, p, sz, i, i, i, p]),
+            "APE_LZ4_socket_stats": (i, [p, i]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -390,3 +392,17 @@ def socket_recv_blocks(fd, dst, block_size, batch, results):
     if r < 0:
         raise GpuError("APE_LZ4_socket_recv_blocks failed (%d): %s" % (r, gpu_last_error()))
     return r
+
+
+SOCKET_STATS = {"tx_h2d_ms": 0, "tx_encode_ms": 1, "tx_d2h_ms": 2, "tx_write_ms": 3,
+                "tx_gpu_wait_ms": 4, "tx_batches": 5, "tx_total_ms": 6, "rx_total_ms": 7,
+                "rx_read_ms": 8, "rx_parse_ms": 9, "rx_h2d_ms": 10, "rx_decode_ms": 11,
+                "rx_d2h_ms": 12, "rx_gpu_wait_ms": 13, "rx_batches": 14, "rx_prepare_ms": 15}
+
+
+def socket_stats(reset=True):
+    """APE_LZ4_socket_stats: the time split of the socket calls since the last reset."""
+    out = (_C.c_double * 16)()
+    if lib().APE_LZ4_socket_stats(out, 1 if reset else 0) != 0:
+        raise GpuError("APE_LZ4_socket_stats failed")
+    return {k: round(out[i], 3) for k, i in SOCKET_STATS.items()}

@@ -23,6 +23,8 @@
 //     next.  The event loop is not rebuilt: these are blocking calls for one connection
 //     (a caller runs TX and RX on their own threads, as the loopback benchmark does).
 #include <errno.h>
+#include <time.h>
+#include <atomic>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -70,19 +72,45 @@ long long write_all(int fd, const char *buf, size_t len) {
     return (long long)done;
 }
 
+// Time split of the last socket calls (APE_LZ4_socket_stats): GPU phases from timing
+// events around each batch's stages, host phases from the monotonic clock.
+//   TX: 0 H2D, 1 encode + frame offsets + pack, 2 D2H, 3 write(), 4 waiting for the GPU,
+//       5 batches, 6 the whole call;  RX: 7 the whole loop, 8 read(), 9 frame parse +
+//       leftover copy, 10 H2D, 11 decode, 12 D2H, 13 waiting for the GPU, 14 batches,
+//       15 receive-buffer growth (prepare).   (ns; batches as counts)
+std::atomic<long long> g_sock_ns[16];
+inline long long now_ns() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (long long)ts.tv_sec * 1000000000ll + ts.tv_nsec;
+}
+inline void sock_add(int i, long long v) { g_sock_ns[i].fetch_add(v, std::memory_order_relaxed); }
+
 struct Dev {   // device buffers of one batch slot
     char *src = nullptr, *comp = nullptr, *frames = nullptr, *out = nullptr;
     int *csz = nullptr, *sizes = nullptr, *res = nullptr;
     long long *off = nullptr;
+    int *hres = nullptr;      // RX: pinned landing slot of the batch's results (a D2H into
+                              // the caller's pageable array would block the receive loop)
     void *scratch = nullptr;
     hipStream_t st = nullptr;
     hipEvent_t ev = nullptr;
+    hipEvent_t tev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // stage timing
 };
+
+// elapsed ns between timing events a and b (both complete)
+inline long long ev_ns(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    return hipEventElapsedTime(&ms, a, b) == hipSuccess ? (long long)(ms * 1e6) : 0;
+}
 
 int dev_alloc(Dev &d, int batch, int bs, bool tx) {
     const size_t slot = up16((size_t)bound_of(bs));
     bool ok = hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&d.ev, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreate(&d.tev[0]) == hipSuccess && hipEventCreate(&d.tev[1]) == hipSuccess &&
+              hipEventCreate(&d.tev[2]) == hipSuccess && hipEventCreate(&d.tev[3]) == hipSuccess &&
+              hipEventCreate(&d.tev[4]) == hipSuccess &&
               hipMalloc((void **)&d.frames, (size_t)batch * (slot + 4) + 64) == hipSuccess &&
               hipMalloc((void **)&d.off, ((size_t)batch + 1) * sizeof(long long)) == hipSuccess &&
               hipMalloc((void **)&d.sizes, (size_t)batch * sizeof(int)) == hipSuccess;
@@ -93,7 +121,8 @@ int dev_alloc(Dev &d, int batch, int bs, bool tx) {
              hipMalloc(&d.scratch, APE_LZ4_frame_scratch_size(batch) + 16) == hipSuccess;
     if (ok && !tx)
         ok = hipMalloc((void **)&d.out, (size_t)batch * bs) == hipSuccess &&
-             hipMalloc((void **)&d.res, (size_t)batch * sizeof(int)) == hipSuccess;
+             hipMalloc((void **)&d.res, (size_t)batch * sizeof(int)) == hipSuccess &&
+             hipHostMalloc((void **)&d.hres, (size_t)batch * sizeof(int), hipHostMallocDefault) == hipSuccess;
     if (ok) {
         int *h = (int *)malloc((size_t)batch * sizeof(int));
         ok = h != nullptr;
@@ -111,7 +140,10 @@ void dev_free(Dev &d) {
     for (void *p : {(void *)d.src, (void *)d.comp, (void *)d.frames, (void *)d.out, (void *)d.csz,
                     (void *)d.sizes, (void *)d.res, (void *)d.off, d.scratch})
         if (p) (void)hipFree(p);
+    if (d.hres) (void)hipHostFree(d.hres);
     if (d.ev) (void)hipEventDestroy(d.ev);
+    for (hipEvent_t e : d.tev)
+        if (e) (void)hipEventDestroy(e);
     if (d.st) (void)hipStreamDestroy(d.st);
     d = Dev();
 }
@@ -166,6 +198,27 @@ int APE_LZ4_rxbuf_append(APE_LZ4_rxbuf *b, const char *data, size_t len) {
 // header position (i < n), off[n] = the end of the last complete frame.  At most
 // max_frames; a size < 0 or > max_block is malformed: -1 (the stream is unusable, as
 // the reference socket's decode error, src/ape_socket.c:1393-1396).
+namespace {
+// frames_from: APE_LZ4_rxbuf_frames continued after the `n0` frames already found in
+// off[0..n0] (off[n0] = where parsing stopped), so a receiver that reads a batch in many
+// pieces parses each frame once
+int frames_from(const APE_LZ4_rxbuf *b, long long *off, int n0, int max_frames, int max_block) {
+    size_t pos = n0 ? (size_t)off[n0] : 0;
+    int n = n0;
+    while (n < max_frames && b->used - pos >= 4) {
+        const unsigned char *h = (const unsigned char *)b->data + pos;
+        const uint32_t sz = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) |
+                            ((uint32_t)h[3] << 24);
+        if ((int32_t)sz < 0 || (int32_t)sz > max_block) return -1;
+        if (b->used - pos - 4 < sz) break;   // the block is not all here yet
+        off[n++] = (long long)pos;
+        pos += 4 + (size_t)sz;
+    }
+    off[n] = (long long)pos;
+    return n;
+}
+}  // namespace
+
 int APE_LZ4_rxbuf_frames(const APE_LZ4_rxbuf *b, long long *off, int max_frames, int max_block) {
     if (!b || !off || max_frames < 0) return -1;
     size_t pos = 0;
@@ -229,34 +282,49 @@ long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_strid
         const int k = nblocks - c * batch < batch ? nblocks - c * batch : batch;
         nb[c & 1] = k;
         const char *src = h_src + (size_t)c * batch * src_stride;
+        (void)hipEventRecord(D.tev[0], D.st);
         hipError_t e = hipMemcpy2DAsync(D.src, (size_t)block_size, src, src_stride, (size_t)block_size,
                                         (size_t)k, hipMemcpyHostToDevice, D.st);
         if (e != hipSuccess) return APE_LZ4_GPU_ELAUNCH;
+        (void)hipEventRecord(D.tev[1], D.st);
         int r = APE_LZ4_compress_batch_strided_dev(D.src, (size_t)block_size, D.sizes, D.comp, slot,
                                                    nullptr, D.csz, k, D.st);
         if (r == 0) r = APE_LZ4_frame_offsets_dev(D.csz, D.off, D.scratch, k, D.st);
         if (r == 0) r = APE_LZ4_frame_pack_strided_dev(D.comp, slot, D.csz, D.off, D.frames, k, D.st);
         if (r) return r;
+        (void)hipEventRecord(D.tev[2], D.st);
         e = hipMemcpyAsync(htot[c & 1], D.off + k, sizeof(long long), hipMemcpyDeviceToHost, D.st);
         if (e == hipSuccess) e = hipEventRecord(D.ev, D.st);
         return e == hipSuccess ? 0 : APE_LZ4_GPU_ELAUNCH;
     };
+    const long long ttx = now_ns();
     if (rc == 0 && nbat > 0) rc = launch(0);
     for (int c = 0; c < nbat && rc == 0; c++) {
         Dev &D = d[c & 1];
+        long long t0 = now_ns();
         if (hipEventSynchronize(D.ev) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
         const long long tot = *htot[c & 1];
+        (void)hipEventRecord(D.tev[3], D.st);
         if (hipMemcpyAsync(hf[c & 1], D.frames, (size_t)tot, hipMemcpyDeviceToHost, D.st) != hipSuccess ||
-            hipStreamSynchronize(D.st) != hipSuccess) {
+            hipEventRecord(D.tev[4], D.st) != hipSuccess || hipStreamSynchronize(D.st) != hipSuccess) {
             rc = APE_LZ4_GPU_ELAUNCH;
             break;
         }
+        long long t1 = now_ns();
+        sock_add(4, t1 - t0);
+        sock_add(0, ev_ns(D.tev[0], D.tev[1]));
+        sock_add(1, ev_ns(D.tev[1], D.tev[2]));
+        sock_add(2, ev_ns(D.tev[3], D.tev[4]));
+        sock_add(5, 1);
         if (c + 1 < nbat) rc = launch(c + 1);   // the next batch's GPU work under this write
         if (rc) break;
+        t0 = now_ns();
         const long long w = write_all(fd, hf[c & 1], (size_t)tot);
+        sock_add(3, now_ns() - t0);
         if (w < 0) { rc = APE_LZ4_GPU_EINVAL; break; }
         sent += w;
     }
+    sock_add(6, now_ns() - ttx);
     for (int i = 0; i < 2; i++) {
         dev_free(d[i]);
         if (hf[i]) (void)hipHostFree(hf[i]);
@@ -278,11 +346,13 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
     int rc = APE_LZ4_gpu_init();
     if (rc) return rc;
     const int maxc = bound_of(block_size);
-    const size_t chunk = 1u << 20;   // read() granularity
+    const size_t chunk = 4u << 20;   // read() granularity
     Dev d[2];
     APE_LZ4_rxbuf *rb[2] = {APE_LZ4_rxbuf_new(4u << 20), APE_LZ4_rxbuf_new(4u << 20)};
     long long *hoff[2] = {nullptr, nullptr};
     bool busy[2] = {false, false};
+    long long base[2] = {0, 0};   // first block of the batch in flight on d[i]
+    int cnt[2] = {0, 0};          // ... and its block count
     for (int i = 0; i < 2 && rc == 0; i++) {
         if (!rb[i] || dev_alloc(d[i], batch, block_size, false) != 0 ||
             hipHostMalloc((void **)&hoff[i], ((size_t)batch + 1) * sizeof(long long),
@@ -290,17 +360,26 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
             rc = APE_LZ4_GPU_ENOMEM;
     }
     long long done = 0;       // blocks handed to the GPU
+    const long long trx = now_ns();
     int cur = 0;              // rxbuf receiving
+    int parsed = 0;           // complete frames already found in rb[cur]
     bool eof = false;
     while (rc == 0 && done < nblocks) {
         APE_LZ4_rxbuf *b = rb[cur];
         const int want = nblocks - done < batch ? (int)(nblocks - done) : batch;
-        const int n = APE_LZ4_rxbuf_frames(b, hoff[cur], want, maxc);
+        long long t0 = now_ns();
+        const int n = frames_from(b, hoff[cur], parsed, want, maxc);
+        sock_add(9, now_ns() - t0);
         if (n < 0) { rc = APE_LZ4_GPU_EINVAL; break; }
+        parsed = n;
         if (n < want) {   // read more
             if (eof) { rc = APE_LZ4_GPU_EINVAL; break; }
+            t0 = now_ns();
             if (APE_LZ4_rxbuf_prepare(b, chunk) != 0) { rc = APE_LZ4_GPU_ENOMEM; break; }
+            sock_add(15, now_ns() - t0);
+            t0 = now_ns();
             const ssize_t r = read(fd, b->data + b->used, b->size - b->used);
+            sock_add(8, now_ns() - t0);
             if (r < 0) {
                 if (errno == EINTR) continue;
                 rc = APE_LZ4_GPU_EINVAL;
@@ -313,31 +392,58 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
         // a full batch: hand this buffer to the GPU, continue receiving in the other one
         const int nxt = cur ^ 1;
         if (busy[nxt]) {
+            t0 = now_ns();
             if (hipStreamSynchronize(d[nxt].st) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+            sock_add(13, now_ns() - t0);
+            Dev &P = d[nxt];
+            sock_add(10, ev_ns(P.tev[0], P.tev[1]));
+            sock_add(11, ev_ns(P.tev[1], P.tev[2]));
+            sock_add(12, ev_ns(P.tev[2], P.tev[3]));
+            sock_add(14, 1);
+            memcpy(h_result + base[nxt], P.hres, (size_t)cnt[nxt] * sizeof(int));
             busy[nxt] = false;
         }
         const size_t end = (size_t)hoff[cur][n];
         APE_LZ4_rxbuf *o = rb[nxt];
         o->used = 0;
+        t0 = now_ns();
         if (APE_LZ4_rxbuf_append(o, b->data + end, b->used - end) != 0) { rc = APE_LZ4_GPU_ENOMEM; break; }
+        sock_add(9, now_ns() - t0);
         b->used = end;
         Dev &D = d[cur];
+        (void)hipEventRecord(D.tev[0], D.st);
         hipError_t e = hipMemcpyAsync(D.frames, b->data, end, hipMemcpyHostToDevice, D.st);
         if (e == hipSuccess)
             e = hipMemcpyAsync(D.off, hoff[cur], ((size_t)n + 1) * sizeof(long long),
                                hipMemcpyHostToDevice, D.st);
         if (e != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        (void)hipEventRecord(D.tev[1], D.st);
         rc = APE_LZ4_decompress_safe_frames_dev(D.frames, D.off, D.out, (size_t)block_size, D.sizes,
                                                 D.res, n, D.st);
         if (rc) break;
+        (void)hipEventRecord(D.tev[2], D.st);
         e = hipMemcpy2DAsync(h_dst + (size_t)done * dst_stride, dst_stride, D.out, (size_t)block_size,
                              (size_t)block_size, (size_t)n, hipMemcpyDeviceToHost, D.st);
         if (e == hipSuccess)
-            e = hipMemcpyAsync(h_result + done, D.res, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, D.st);
+            e = hipMemcpyAsync(D.hres, D.res, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, D.st);
+        if (e == hipSuccess) e = hipEventRecord(D.tev[3], D.st);
         if (e != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
         busy[cur] = true;
+        base[cur] = done;
+        cnt[cur] = n;
         done += n;
         cur = nxt;
+        parsed = 0;
+    }
+    sock_add(7, now_ns() - trx);
+    for (int i = 0; i < 2; i++) {   // the last batches' stage times
+        if (rc == 0 && busy[i] && hipStreamSynchronize(d[i].st) == hipSuccess) {
+            sock_add(10, ev_ns(d[i].tev[0], d[i].tev[1]));
+            sock_add(11, ev_ns(d[i].tev[1], d[i].tev[2]));
+            sock_add(12, ev_ns(d[i].tev[2], d[i].tev[3]));
+            sock_add(14, 1);
+            memcpy(h_result + base[i], d[i].hres, (size_t)cnt[i] * sizeof(int));
+        }
     }
     for (int i = 0; i < 2; i++) {
         dev_free(d[i]);
@@ -345,6 +451,17 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
         if (hoff[i]) (void)hipHostFree(hoff[i]);
     }
     return rc ? rc : done;
+}
+
+// Time split of the socket calls since the last reset (see g_sock_ns): out[16] in ms
+// (the two batch counts as counts).  reset != 0 zeroes the accumulators afterwards.
+int APE_LZ4_socket_stats(double *out, int reset) {
+    if (!out) return APE_LZ4_GPU_EINVAL;
+    for (int i = 0; i < 16; i++) {
+        const long long v = reset ? g_sock_ns[i].exchange(0) : g_sock_ns[i].load();
+        out[i] = (i == 5 || i == 14) ? (double)v : (double)v * 1e-6;
+    }
+    return 0;
 }
 
 }  // extern "C"

@@ -356,6 +356,14 @@ int main(int argc, char **argv)
                    (double)n * nb / tot);
         }
     }
+    for (int lag = 3; lag <= 6; lag++) {
+        long tot = 0;
+        g_tsize = 6912;
+        for (int b = 0; b < nb; b++) tot += model4(buf + (size_t)b * n, n, lag, 7, 6, 1 << 20);
+        printf("kernel policy pol 7, table 6912, lag %d                   ratio %.4f\n", lag,
+               (double)n * nb / tot);
+        g_tsize = 8192;
+    }
     {
         const int ts[] = {8192, 7552, 7168, 7040, 6656, 6144, 4096};
         for (unsigned k = 0; k < sizeof(ts) / sizeof(ts[0]); k++) {
