@@ -857,8 +857,152 @@ lz4_decode_kernel(BlockArgs a) {
     STATS_FLUSH(g_dec_stats);
 }
 
+#ifdef APE_LZ4_DEC_COOP
+// ---- Experiment (never the product): two waves per block, pipelined ----
+// Wave 0 parses batch k+1 while wave 1 copies batch k: descriptors move from the parser's
+// LDS to the copier's at a handoff between two workgroup barriers; the copier stages the
+// compressed bytes of its batch's literals itself and owns the output window.
+struct CoopLds {
+    WaveLds p, c;    // parser: stage + descriptors (its window unused); copier: all three
+    uint32_t hdr[4];   // handoff: {nc, B0, B1, flags (1 last, 2 end)}
+};
+
+template <bool PARTIAL, bool DICT, bool FASTD>
+__global__ void __launch_bounds__(128)
+lz4_decode_coop_kernel(BlockArgs a) {
+    __shared__ CoopLds S;
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool parser = threadIdx.x < 64;
+    Dec D;
+    D.dst = (gu8 *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
+    if (a.frame_off) {
+        const long long f0 = a.frame_off[b], avail = a.frame_off[b + 1] - f0 - 4;
+        int hdr = -1;
+        gcu8 *f = (gcu8 *)(a.src_base + f0);
+        if (avail >= 0)
+            hdr = (int)((uint32_t)f[0] | ((uint32_t)f[1] << 8) | ((uint32_t)f[2] << 16) |
+                        ((uint32_t)f[3] << 24));
+        if (hdr < 0 || (long long)hdr > avail) {
+            if (threadIdx.x == 0) a.result[b] = -1;
+            return;
+        }
+        D.csize = hdr;
+        D.src = f + 4;
+    } else {
+        D.src = (gcu8 *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
+        D.csize = a.src_size[b];
+    }
+    D.cap = a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride;
+    D.oexit = PARTIAL ? a.target[b] : 0;
+    if (PARTIAL && D.oexit > (int64_t)D.cap - kMFLimit) D.oexit = (int64_t)D.cap - kMFLimit;
+    D.lane = lane;
+    D.dend = nullptr;
+    D.dsz = 0;
+    if (DICT) {
+        const int ds = a.dict_size[b] > 0 ? a.dict_size[b] : 0;
+        D.dend = (gcu8 *)a.dict[b] + ds;
+        D.dsz = ds < 65536 ? (uint32_t)ds : 65536u;
+    }
+    if (FASTD && (D.cap == 0 || D.csize <= 0)) {
+        if (threadIdx.x == 0) a.result[b] = (D.cap == 0 && D.csize > 0 && D.src[0] == 0) ? 1 : -1;
+        return;
+    }
+    if (D.cap == 0 || D.csize <= 0) {
+        if (threadIdx.x == 0) {
+            int r;
+            if (D.cap == 0) r = (D.csize == 1 && D.src[0] == 0) ? 0 : -1;
+            else r = ((D.src ? D.src[0] : 0u) >= 0xF0) ? -3 : -2;
+            a.result[b] = r;
+        }
+        return;
+    }
+    WaveLds &L = parser ? S.p : S.c;
+    if (lane < 4) *(uint32_t *)&L.stage[kStage + 4 * lane] = 0u;
+    D.s0 = stage_base(D.src, 0);
+    if (parser) stage_load(L, D.src, D.csize, D.s0, lane);
+    wave_sync();
+    if (D.cap < 0) {   // as in lz4_decode_kernel
+        if (parser) {
+            int ip = 0, nd = 0, result = 0;
+            uint32_t op0 = 0;
+            (void)parse_scalar<PARTIAL, FASTD>(L, D, ip, op0, nd, result);
+            if (lane == 0) a.result[b] = result;
+        }
+        return;
+    }
+    if (parser) {
+        int P = 0, nd = 0, result = 0, st = ST_MORE;
+        uint32_t op = 0, cst = 0;
+        for (;;) {
+            while (st == ST_MORE && nd < kBatch) {
+                if (P - D.s0 + kWinNeed > kStage) {
+                    wave_sync();
+                    D.s0 = stage_base(D.src, P);
+                    stage_load(L, D.src, D.csize, D.s0, lane);
+                    wave_sync();
+                }
+                bool cplx;
+                st = parse_window<PARTIAL, DICT, FASTD>(L, D, P, op, nd, result, cplx);
+                if (st == ST_MORE && cplx) st = parse_scalar<PARTIAL, FASTD>(L, D, P, op, nd, result);
+            }
+            wave_sync();
+            const int nc = st == ST_ERR ? 0 : (nd < kBatch ? nd : kBatch);
+            const uint32_t B1 = nc < nd ? (uint32_t)__builtin_amdgcn_readfirstlane(L.desc[nc].y) : op;
+            const bool last = st == ST_DONE && nc == nd;
+            const bool end = st == ST_ERR || last;
+            const uint4 dv = L.desc[lane < nc ? lane : 0];
+            const uint4 cv = L.desc[nc + (lane < nd - nc ? lane : 0)];
+            __syncthreads();   // (1) the copier is done with its descriptors
+            if (lane < nc) S.c.desc[lane] = dv;
+            if (lane == 0) {
+                S.hdr[0] = (uint32_t)nc;
+                S.hdr[1] = cst;
+                S.hdr[2] = B1;
+                S.hdr[3] = (last ? 1u : 0u) | (end ? 2u : 0u);
+            }
+            if (nc < nd && lane < nd - nc) L.desc[lane] = cv;
+            nd -= nc;
+            cst = B1;
+            __syncthreads();   // (2) batch handed over
+            if (end) break;
+        }
+        if (lane == 0) a.result[b] = result;
+    } else {
+        Win W;
+        W.base = 0;
+        W.fl = 0;
+        W.gdone = 0;
+        for (;;) {
+            __syncthreads();   // (1)
+            __syncthreads();   // (2)
+            const int nc = (int)__builtin_amdgcn_readfirstlane(S.hdr[0]);
+            const uint32_t B0 = __builtin_amdgcn_readfirstlane(S.hdr[1]);
+            const uint32_t B1 = __builtin_amdgcn_readfirstlane(S.hdr[2]);
+            const uint32_t fl = __builtin_amdgcn_readfirstlane(S.hdr[3]);
+            const bool last = (fl & 1u) != 0u;
+            if (nc > 0 || last) {
+                if (nc > 0) {   // this batch's literals, staged from its first one on
+                    D.s0 = stage_base(D.src, (int)__builtin_amdgcn_readfirstlane(L.desc[0].x));
+                    stage_load(L, D.src, D.csize, D.s0, lane);
+                }
+                uint32_t diag = 0;
+                copy_batch<DICT>(L, D, W, nc, B0, B1, last, diag);
+            }
+            if (fl & 2u) break;
+        }
+    }
+}
+#endif
+
 hipError_t launch_decode(const BlockArgs &a, bool partial, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
+#ifdef APE_LZ4_DEC_COOP
+    if (!a.fast && !a.dict && !partial) {
+        hipLaunchKernelGGL((lz4_decode_coop_kernel<false, false, false>), dim3(a.nblocks), dim3(128), 0, s, a);
+        return hipGetLastError();
+    }
+#endif
     if (a.fast)   // decompress_fast (ref :1489)
         hipLaunchKernelGGL((lz4_decode_kernel<false, false, true>), dim3(a.nblocks), dim3(64), 0, s, a);
     else if (a.dict)   // usingDict decodes are full decodes (ref :1625-1647)

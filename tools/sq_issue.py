@@ -22,12 +22,12 @@ SIMDS, CLK = 1024, 2.4e9
 
 
 def kind(name):
-    return "lz4_encode_kernel" if "encode" in name else ("lz4_decode_kernel" if "decode" in name else None)
+    return "lz4_encode_kernel" if "encode" in name else (("lz4_decode_coop_kernel" if "coop" in name else "lz4_decode_kernel") if "decode" in name else None)
 
 
 def main():
     nb = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
-    base = os.path.join(ROOT, "gpurun_out", "sq")
+    base = os.environ.get("SQ_DIR", os.path.join(ROOT, "gpurun_out", "sq"))
     cnt = collections.defaultdict(dict)
     dur = collections.defaultdict(list)
     for p in sorted(glob.glob(os.path.join(base, "p*"))):
@@ -61,9 +61,9 @@ def main():
                 round(c.get("SQ_INSTS_SALU", 0) / units, 1),
             "counters": {n: v for n, v in sorted(c.items())},
         }
-    with open(os.path.join(ROOT, "profiles", "sq_issue.json"), "w") as f:
+    with open(os.path.join(ROOT, "profiles", os.environ.get("SQ_JSON", "sq_issue.json")), "w") as f:
         json.dump(out, f, indent=1)
-    for k in ("lz4_encode_kernel", "lz4_decode_kernel"):
+    for k in ("lz4_encode_kernel", "lz4_decode_kernel", "lz4_decode_coop_kernel"):
         if k in out:
             print(k, {a: b for a, b in out[k].items() if a != "counters"})
 
