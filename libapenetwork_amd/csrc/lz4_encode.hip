@@ -76,6 +76,9 @@ static_assert(kHSize <= (1 << kHLog) && kHSize % 8 == 0, "table size");
 #ifndef APE_LZ4_WAVES_PER_EU
 #define APE_LZ4_WAVES_PER_EU 7
 #endif
+#ifndef APE_LZ4_HOP_ASM
+#define APE_LZ4_HOP_ASM 1
+#endif
 #ifndef APE_LZ4_EAGER_T
 #define APE_LZ4_EAGER_T 16
 #endif
@@ -142,7 +145,7 @@ __device__ __forceinline__ void vm_wait() {
 }
 
 // Diagnostic (sensitivity A/B only, never the product): N dependent-free 4-cycle VALU ops
-// (APE_EXP_PAD_P / _W / _PL: producer, walker VALU; producer LDS reads).
+// (APE_EXP_PAD_P / _W / _E / _PL: producer, walker, emitter VALU; producer LDS reads).
 template <int N>
 __device__ __forceinline__ void pad_valu(uint32_t &x) {
 #pragma unroll
@@ -165,6 +168,9 @@ __device__ __forceinline__ void pad_lds(uint32_t &x) {
 #endif
 #ifndef APE_EXP_PAD_PL
 #define APE_EXP_PAD_PL 0
+#endif
+#ifndef APE_EXP_PAD_E
+#define APE_EXP_PAD_E 0
 #endif
 
 __device__ __forceinline__ void wave_sync() {
@@ -719,6 +725,60 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     const uint32_t Lh = iv.x & 0xFFu;                     // hop; | 0x80 = unfinished
     uint32_t rel = W.q - P;
     uint64_t M = 0;
+    if constexpr (!ACC) {
+        // The hop chain with one v_readlane per member: nxt = the walk position after the
+        // lane's match (+256 marks a match the producer could not finish), so that a hop is
+        // shift, find-first, add, readlane, compare.
+        const uint32_t nxt = (uint32_t)lane + (iv.x & 0x7Fu) + ((iv.x & 0x80u) << 1);
+        for (;;) {
+#if APE_LZ4_HOP_ASM
+            // shift, find-first, add, mark, readlane, compare, branch: 9 scalar-unit
+            // instructions per member (the compiler's loop took 13); leaves with rel >= 64
+            // (64: no match lane left)
+            uint32_t j;
+            uint64_t t;
+            asm volatile(
+                "1:\n\t"
+                "s_lshr_b64 %[t], %[hm], %[rel]\n\t"
+                "s_cmp_eq_u64 %[t], 0\n\t"
+                "s_cbranch_scc1 2f\n\t"
+                "s_ff1_i32_b64 %[j], %[t]\n\t"
+                "s_add_u32 %[j], %[j], %[rel]\n\t"
+                "s_bitset1_b64 %[m], %[j]\n\t"
+                "v_readlane_b32 %[rel], %[nxt], %[j]\n\t"
+                "s_cmp_lt_u32 %[rel], 64\n\t"
+                "s_cbranch_scc1 1b\n\t"
+                "s_branch 3f\n"
+                "2:\n\t"
+                "s_mov_b32 %[rel], 64\n"
+                "3:"
+                : [rel] "+s"(rel), [m] "+s"(M), [j] "=&s"(j), [t] "=&s"(t)
+                : [hm] "s"(Hm), [nxt] "v"(nxt)
+                : "scc");
+            if (rel < 256u) break;
+#else
+            const uint64_t w = Hm >> rel;
+            if (w == 0) {   // no match lane left in the chunk
+                rel = 64u;
+                break;
+            }
+            const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
+            M |= 1ull << j;
+            rel = lane_val(nxt, (int)j);
+            if (rel < 64u) continue;
+            if (rel < 256u) break;
+#endif
+            const uint32_t me = P + j;   // unfinished (rare): the wave extends it
+            const uint32_t cm = me - (lane_val(iv.y, (int)j) & 0xFFFFu);
+            const uint32_t Le = extend_match(B, me, cm, rel - 256u - j, lane);
+            if ((uint32_t)lane == j) O.Lf = Le;
+            rel = j + Le;
+            if (rel >= 64u) break;
+        }
+        O.members = M;
+        W.q = P + rel;
+        return;
+    }
     for (;;) {
         // acceleration (:591-600): after a match end e the reference tests e (:710-720),
         // then searches from e+1 with step 1 once and then step = acceleration (without
@@ -1193,6 +1253,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         } else {
             emit_step(S, B, lane, E);
         }
+        if (APE_EXP_PAD_E) { uint32_t x = (uint32_t)lane; pad_valu<APE_EXP_PAD_E>(x); (void)x; }
         STAT(2);
         __syncthreads();
         STAT(14);
