@@ -424,7 +424,9 @@ struct Blk {
 struct Part {                        // C1 result of one chunk, finished by C2
     uint32_t len, c, bk, lim, h, base;   // base: bytes C1 measured (kEagerLen / kEagerL)
     uint32_t rank, ntr, eo;          // stage-2 queue rank, queue size, own bytes of the group
-    bool has, hashable, trunc1;
+    bool has, hashable;
+    uint64_t tmask;                  // lanes whose candidate reached its measured length (a
+                                     // wave mask: no per-lane 0/1 to materialise)
 };
 
 // One parity of the producer pipeline (the step loop is unrolled by two, so no
@@ -471,8 +473,8 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
                                             const uint32_t (&X)[2], uint32_t &cT, uint32_t &jL,
                                             uint32_t &h, uint32_t (&Y)[6]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-    const bool live = k < B.nch;
-    const bool hashable = live && p + 5u <= B.un;
+    // (FAST: chunk k lies inside the block with room to spare, every lane is hashable)
+    const bool hashable = FAST || (k < B.nch && p + 5u <= B.un);
     h = hash5(X[0], X[1]);
     cT = S.tab[h];
     jL = 0xFFFFFFFFu;
@@ -490,9 +492,10 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
 // R(k): ring copy of chunk k (own bytes for C1 and stage 2, match_end - 2, literals; zero
 // past the block end), in the second half of step k - 3, so that C1(k - 1)'s ring read can
 // start a step later without waiting for anything
+template <bool FAST = false>
 __device__ __forceinline__ void prod_ring(EncLds &S, const Blk &B, int k, int lane,
                                           const uint32_t (&X)[2]) {
-    if (k < B.nch) {
+    if (FAST || k < B.nch) {
         const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
         const uint8_t by = (uint8_t)X[0];
         ((uint8_t *)S.ring)[p & (kRingE - 1)] = by;
@@ -527,7 +530,7 @@ __device__ __forceinline__ void prod_own(const EncLds &S, int k, int lane, uint3
 __device__ __forceinline__ bool stage2_group(const Part &R, int lane, uint32_t first, uint32_t p,
                                              uint32_t &cb, uint32_t &eo) {
     const uint32_t r = R.rank - first, i16 = 16u * ((uint32_t)lane & 3u);
-    const bool push = R.trunc1 && r < kGroups;
+    const bool push = lane_in(R.tmask) && r < kGroups;
     const int tgt = (int)((push ? 4u * r : ((uint32_t)lane | 1u)) << 2);
     cb = dpp<0x00>(0u, (uint32_t)__builtin_amdgcn_ds_permute(tgt, (int)(R.c + R.base))) + i16;
     eo = dpp<0x00>(0u, (uint32_t)__builtin_amdgcn_ds_permute(tgt, (int)(p + R.base))) + i16;
@@ -563,11 +566,15 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     }
     const uint32_t (&Yr)[6] = kWin ? Yw : Y;
 #define Y Yr
-    const bool live = k < B.nch;
-    R.hashable = live && p + 5u <= B.un;
-    const bool can = live && p >= 1u && p <= B.mstart && B.n >= kMinLength;
+    // FAST (chunk k + 1 lies inside the block with 83 bytes to spare, k >= 1): every lane is
+    // live, hashable and may start a match
+    const bool live = FAST || k < B.nch;
+    R.hashable = FAST || (live && p + 5u <= B.un);
+    const bool can = FAST || (live && p >= 1u && p <= B.mstart && B.n >= kMinLength);
     const uint32_t cL = 64u * (uint32_t)k + jL;
-    // L candidate bytes in[cL-4, cL+12) from lane jL's own bytes
+    // L candidate bytes in[cL-4, cL+12) from lane jL's own bytes (4 ds_bpermute; reading
+    // them from the ring beside X, in the same LDS round trip, measured +2.3 % encode time:
+    // 5 ds_read + 4 v_alignbyte)
     uint32_t Z[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) Z[t] = bperm(X[t], jL);
@@ -587,7 +594,7 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     R.c = pickL ? cL : cT;
     R.len = pickL ? lL : lT;
     R.base = pickL ? kEagerL : kEagerLen;
-    R.trunc1 = (R.len >= R.base) & (R.lim > R.base);
+    R.tmask = wave_ballot((R.len >= R.base) & (R.lim > R.base));
     R.len = umin(R.len, R.lim);
     R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
     R.has = okT | okL;
@@ -601,7 +608,7 @@ template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_stage2_issue(const EncLds &S, const Blk &B, int k, int lane,
                                                   Part &R, uint32_t (&E)[4]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-    const uint64_t tb = wave_ballot(R.trunc1);
+    const uint64_t tb = R.tmask;
     R.ntr = (uint32_t)__popcll(tb);
     R.rank = lane_rank(tb);
     uint32_t cb;
@@ -636,7 +643,7 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
             const uint32_t m2 = bperm(stage2_len(S, lane, eo, E2), 4u * (R.rank - first));
             if (R.rank - first < kGroups) mine = m2;
         }
-        if (R.trunc1) {
+        if (lane_in(R.tmask)) {
             len = umin(R.base + mine, R.lim);
             trunc = mine == kExt2 && R.lim > R.base + kExt2;
         }
@@ -706,6 +713,7 @@ struct WalkOut {
     uint32_t m_back, m_len, an;   // per member lane
     uint2 iv;
     uint32_t q0, Lf;              // walk start; forward match length per lane
+    uint2 e2v;                    // in[e2, e2 + 8), e2 = match_end - 2 (read before the walk)
 };
 
 // First half: the hop chain only (the latency-bound part); second half, before the
@@ -719,6 +727,11 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     O.iv = S.info[k & 1][lane];
     O.q0 = W.q;
     O.Lf = O.iv.x & 0x7Fu;                               // forward match length
+    // match_end - 2 (:680) of every lane's match, read from the ring now so that the
+    // second half's hash needs no LDS round trip (the ring holds chunks k - 12 .. k + 3,
+    // and a match the producer finished ends before p + 81; a match the walker extends
+    // is hashed from the input instead)
+    O.e2v = ring8(S, P + (uint32_t)lane + O.Lf - 2u);
     if (W.q >= P + 64u) return;               // a match from earlier chunks covers it
     const uint2 iv = O.iv;
     const uint64_t Hm = wave_ballot(O.Lf != 0u);          // lanes with a match
@@ -851,14 +864,13 @@ __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int
     const bool mem = lane_in(O.members);
     const uint32_t fwd = O.m_len - O.m_back;      // match length from p
     // match_end - 2 (:680) of the members, hashed here (off the producer's chain): from the
-    // ring -- it holds chunks k - 12 .. k + 3 now, and a match the producer finished ends
-    // before p + 81 -- or, for a match the walker extended, from the input
+    // ring bytes read before the walk, or, for a match the walker extended, from the input
     const uint32_t e2 = p + fwd - 2u;
     const bool e2ok = mem && e2 + 5u <= B.un;
     uint32_t e2h = 0;
     if (e2ok) {
         if (!(iv.x & I_TRUNC)) {
-            const uint2 v = ring8(S, e2);
+            const uint2 v = O.e2v;   // read before the walk (-1.6 % encode time)
             e2h = hash5(v.x, v.y);
         } else {
             uint32_t lo32 = 0, b4 = 0;
@@ -1148,7 +1160,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             STAT(7);
             vm_wait<kWin ? 0 : 3>();
             STAT(9);
-            prod_ring(S, B, s + 3, lane, nxt.X);
+            prod_ring<F>(S, B, s + 3, lane, nxt.X);
             prod_finish<SMALL, F>(S, B, s, lane, cur.q, cur.E);
             STAT(7);
             __syncthreads();
