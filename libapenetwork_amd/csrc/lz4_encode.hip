@@ -76,9 +76,6 @@ static_assert(kHSize <= (1 << kHLog) && kHSize % 8 == 0, "table size");
 #ifndef APE_LZ4_WAVES_PER_EU
 #define APE_LZ4_WAVES_PER_EU 7
 #endif
-#ifndef APE_LZ4_HOP_ASM
-#define APE_LZ4_HOP_ASM 1
-#endif
 #ifndef APE_LZ4_EAGER_T
 #define APE_LZ4_EAGER_T 16
 #endif
@@ -716,6 +713,33 @@ struct WalkOut {
     uint2 e2v;                    // in[e2, e2 + 8), e2 = match_end - 2 (read before the walk)
 };
 
+// The walker's hop chain from walk position rel (< 64): shift, find-first, add, mark,
+// v_readlane, compare, branch -- 9 scalar-unit instructions per member (the compiler's loop
+// took 13).  nxt (per lane) = the walk position after the lane's match; leaves with rel >= 64
+// (64: no match lane left), j = the last member, its bit set in M.
+__device__ __forceinline__ void hop_chain(uint64_t Hm, uint32_t nxt, uint32_t &rel, uint64_t &M,
+                                          uint32_t &j) {
+    uint64_t t;
+    asm volatile(
+        "1:\n\t"
+        "s_lshr_b64 %[t], %[hm], %[rel]\n\t"
+        "s_cmp_eq_u64 %[t], 0\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "s_ff1_i32_b64 %[j], %[t]\n\t"
+        "s_add_u32 %[j], %[j], %[rel]\n\t"
+        "s_bitset1_b64 %[m], %[j]\n\t"
+        "v_readlane_b32 %[rel], %[nxt], %[j]\n\t"
+        "s_cmp_lt_u32 %[rel], 64\n\t"
+        "s_cbranch_scc1 1b\n\t"
+        "s_branch 3f\n"
+        "2:\n\t"
+        "s_mov_b32 %[rel], 64\n"
+        "3:"
+        : [rel] "+s"(rel), [m] "+s"(M), [j] "+s"(j), [t] "=&s"(t)
+        : [hm] "s"(Hm), [nxt] "v"(nxt)
+        : "scc");
+}
+
 // First half: the hop chain only (the latency-bound part); second half, before the
 // inserts: the lane-parallel catch-up limits, walked set and anchor (walk_finish).
 template <bool ACC>
@@ -740,53 +764,18 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     uint64_t M = 0;
     if constexpr (!ACC) {
         // The hop chain with one v_readlane per member: nxt = the walk position after the
-        // lane's match (+256 marks a match the producer could not finish), so that a hop is
-        // shift, find-first, add, readlane, compare.
+        // lane's match, +256 marking a match the producer could not finish.
         const uint32_t nxt = (uint32_t)lane + (iv.x & 0x7Fu) + ((iv.x & 0x80u) << 1);
-        for (;;) {
-#if APE_LZ4_HOP_ASM
-            // shift, find-first, add, mark, readlane, compare, branch: 9 scalar-unit
-            // instructions per member (the compiler's loop took 13); leaves with rel >= 64
-            // (64: no match lane left)
-            uint32_t j;
-            uint64_t t;
-            asm volatile(
-                "1:\n\t"
-                "s_lshr_b64 %[t], %[hm], %[rel]\n\t"
-                "s_cmp_eq_u64 %[t], 0\n\t"
-                "s_cbranch_scc1 2f\n\t"
-                "s_ff1_i32_b64 %[j], %[t]\n\t"
-                "s_add_u32 %[j], %[j], %[rel]\n\t"
-                "s_bitset1_b64 %[m], %[j]\n\t"
-                "v_readlane_b32 %[rel], %[nxt], %[j]\n\t"
-                "s_cmp_lt_u32 %[rel], 64\n\t"
-                "s_cbranch_scc1 1b\n\t"
-                "s_branch 3f\n"
-                "2:\n\t"
-                "s_mov_b32 %[rel], 64\n"
-                "3:"
-                : [rel] "+s"(rel), [m] "+s"(M), [j] "=&s"(j), [t] "=&s"(t)
-                : [hm] "s"(Hm), [nxt] "v"(nxt)
-                : "scc");
-            if (rel < 256u) break;
-#else
-            const uint64_t w = Hm >> rel;
-            if (w == 0) {   // no match lane left in the chunk
-                rel = 64u;
-                break;
-            }
-            const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
-            M |= 1ull << j;
-            rel = lane_val(nxt, (int)j);
-            if (rel < 64u) continue;
-            if (rel < 256u) break;
-#endif
-            const uint32_t me = P + j;   // unfinished (rare): the wave extends it
+        uint32_t j = 0;
+        hop_chain(Hm, nxt, rel, M, j);
+        while (__builtin_expect(rel >= 256u, 0)) {   // unfinished (rare): the wave extends it
+            const uint32_t me = P + j;
             const uint32_t cm = me - (lane_val(iv.y, (int)j) & 0xFFFFu);
             const uint32_t Le = extend_match(B, me, cm, rel - 256u - j, lane);
             if ((uint32_t)lane == j) O.Lf = Le;
             rel = j + Le;
             if (rel >= 64u) break;
+            hop_chain(Hm, nxt, rel, M, j);
         }
         O.members = M;
         W.q = P + rel;
@@ -1211,26 +1200,34 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         W.dense = 3u;   // the first search probes 0, 1, 2, then every stride-th
         WalkOut O;
         __syncthreads();
-        for (int s = k0; s < nsteps; s++) {
+        // chunk s - 1 is walked during step s for s in [k0 + 1, nch]; the first step and
+        // the steps past the last chunk only keep the barrier count (separate loops, so
+        // the walking loop carries no per-step predicate)
 #ifdef APE_EXP_NOWALK
-            const bool work = false;   // diagnostic: instruction count without the walker
+        const int s2 = k0 + 1;   // diagnostic: instruction count without the walker
 #else
-            const bool work = s >= k0 + 1 && s <= nch;
+        const int s2 = nch + 1;
 #endif
-            if (work) walk_chain<ACC>(S, B, s - 1, lane, W, O);
+        __syncthreads();   // step k0
+        __syncthreads();
+        int s = k0 + 1;
+        for (; s < s2; s++) {
+            walk_chain<ACC>(S, B, s - 1, lane, W, O);
             if (APE_EXP_PAD_W) { uint32_t x = (uint32_t)lane; pad_valu<APE_EXP_PAD_W>(x); (void)x; }
             STAT(0);
             __syncthreads();
             STAT(4);
-            if (work) {
-                walk_finish<ACC>(B, s - 1, lane, W, O);
-                walk_publish(S, B, s - 1, lane, O, qn);
-                STAT_ADD(11, __popcll(O.members));
-            }
+            walk_finish<ACC>(B, s - 1, lane, W, O);
+            walk_publish(S, B, s - 1, lane, O, qn);
+            STAT_ADD(11, __popcll(O.members));
             STAT(1);
             STAT_ADD(10, 3);
             __syncthreads();
             STAT(3);
+        }
+        for (; s < nsteps; s++) {
+            __syncthreads();
+            __syncthreads();
         }
         STATS_FLUSH(g_enc_stats);
         return;
