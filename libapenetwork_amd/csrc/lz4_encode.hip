@@ -440,7 +440,7 @@ struct PSet {
 // A(k): own bytes in[p, p+8) for the hash (0 past the block end)
 template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_t (&X)[2]) {
-    const uint32_t pos = (k < B.nch ? 64u * (uint32_t)k : 0u) + (uint32_t)lane;
+    const uint32_t pos = (FAST || k < B.nch ? 64u * (uint32_t)k : 0u) + (uint32_t)lane;
     if (FAST || (!SMALL && 64 * k + 72 <= B.n)) {   // wave-uniform: the whole window is inside
         const uint2 v = gload8(B.in + pos);
         X[0] = v.x;
@@ -460,7 +460,7 @@ template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_fetch_t(const Blk &B, int k, int lane, uint32_t cT,
                                              uint32_t (&Y)[6]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-    const bool tryT = k < B.nch && cT < p && cT >= 4u;
+    const bool tryT = (FAST || k < B.nch) && cT < p && cT >= 4u;
     loadv<kYW>(B.in, B.un, tryT ? cT - 4u : 0u, Y, FAST || (!SMALL && 64 * k + 83 <= B.n));
 }
 
@@ -591,7 +591,9 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     R.c = pickL ? cL : cT;
     R.len = pickL ? lL : lT;
     R.base = pickL ? kEagerL : kEagerLen;
-    R.tmask = wave_ballot((R.len >= R.base) & (R.lim > R.base));
+    // (two ballots of compares fold into the compares; a ballot of their AND made the
+    // compiler materialise a 0/1 and compare it again)
+    R.tmask = wave_ballot(R.len >= R.base) & wave_ballot(R.lim > R.base);
     R.len = umin(R.len, R.lim);
     R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
     R.has = okT | okL;
@@ -711,6 +713,7 @@ struct WalkOut {
     uint2 iv;
     uint32_t q0, Lf;              // walk start; forward match length per lane
     uint2 e2v;                    // in[e2, e2 + 8), e2 = match_end - 2 (read before the walk)
+    uint32_t e2h;                 // its hash
 };
 
 // The walker's hop chain from walk position rel (< 64): shift, find-first, add, mark,
@@ -825,7 +828,11 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
 template <bool ACC>
 __device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk &W, WalkOut &O) {
     const uint32_t P = 64u * (uint32_t)k;
-    if (O.q0 >= P + 64u) return;              // covered by a match from earlier chunks
+    // match_end - 2's hash, from the bytes read before the walk (every lane; a match the
+    // walker extended is rehashed in walk_publish): independent of the scan below, so it
+    // fills the scan's DPP wait states.  (No early exit for a chunk a match from earlier
+    // chunks covers: it has no members, nothing is walked, the anchor stays.)
+    O.e2h = hash5(O.e2v.x, O.e2v.y);
     // catch-up limits: a member's backward extension stops at the previous end
     const uint32_t anchor0 = W.anchor;
     const bool mem = lane_in(O.members);
@@ -856,19 +863,14 @@ __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int
     // ring bytes read before the walk, or, for a match the walker extended, from the input
     const uint32_t e2 = p + fwd - 2u;
     const bool e2ok = mem && e2 + 5u <= B.un;
-    uint32_t e2h = 0;
-    if (e2ok) {
-        if (!(iv.x & I_TRUNC)) {
-            const uint2 v = O.e2v;   // read before the walk (-1.6 % encode time)
-            e2h = hash5(v.x, v.y);
-        } else {
-            uint32_t lo32 = 0, b4 = 0;
-            for (uint32_t t = 0; t < 5u; t++) {
-                const uint32_t by = B.in[e2 + t];
-                if (t < 4) lo32 |= by << (8 * t); else b4 = by;
-            }
-            e2h = hash5(lo32, b4);
+    uint32_t e2h = O.e2h;   // (ring bytes read before the walk: -1.6 % encode time)
+    if (e2ok && (iv.x & I_TRUNC)) {   // rare: a match the walker extended
+        uint32_t lo32 = 0, b4 = 0;
+        for (uint32_t t = 0; t < 5u; t++) {
+            const uint32_t by = B.in[e2 + t];
+            if (t < 4) lo32 |= by << (8 * t); else b4 = by;
         }
+        e2h = hash5(lo32, b4);
     }
     // one wave's LDS operations complete in order: the walked-position inserts above
     // land before these (compiler barrier only)
