@@ -19,6 +19,7 @@
 // lock step, two workgroup barriers per step s (each waits only on its own memory
 // operations; s_waitcnt vmcnt counts a wave's loads and stores together, in order):
 //   PRODUCER (wave 1), three chunks in flight:
+//     R(s+2)  copy chunk s+2 (loaded a step ago) into the ring;
 //     A(s+3)  load in[p, p+8) for every position p of the chunk;
 //     B(s+2)  hash in[p, p+5), read candidate T = table[h] (positions walked
 //             earlier plus match_end - 2, inserted as the reference does:
@@ -28,16 +29,17 @@
 //             bytes and L to 12 forward and both 4 backward, keep the longer;
 //     S2(s+1) (second half) the truncated candidates, ranked and pushed into groups
 //             of 4 lanes, each group loading the 64 bytes that follow;
-//     R(s+3)  copy chunk s+3 into the ring;
 //     C2(s)   finish the truncated lengths (+64 bytes) -> match info of chunk s.
-//   WALKER (wave 0), chunk s-1: the greedy chain on the scalar unit (hops over the
-//     match lanes of a ballot mask), catch-up into pending literals (:623-627),
-//     the wave-wide extension of matches >= 80 bytes; second half: table inserts
-//     of the walked positions and match_end - 2 (:680, hashed here from the ring),
-//     never overlapping B.
-//   EMITTER (wave 2), chunk s-2: sizes and prefix-sum offsets of the sequences,
-//     then each lane of a 64-byte output window computes its output byte; the
-//     last literals (:732-751) are copied with 16-byte moves.
+//   WALKER (wave 0), chunk s-1: the greedy chain on the scalar unit (a 9-instruction
+//     loop over the match lanes of a ballot mask, one v_readlane per member), the
+//     wave-wide extension of matches >= 80 bytes; second half: catch-up into pending
+//     literals (:623-627), table inserts of the walked positions and match_end - 2
+//     (:680, hashed from ring bytes read before the walk), never overlapping B, and the
+//     chunk's sequence records queued for the emitter.
+//   EMITTER (wave 2), every <= 8 steps: up to 64 queued records sized, prefix-summed
+//     and staged in LDS (token, lengths, offset, literals from the ring), then stored
+//     with one 16-byte store per lane; the last literals (:732-751) are copied with
+//     16-byte moves.
 #include "lz4_gpu_internal.h"
 #include <stdlib.h>
 #include <type_traits>
@@ -487,8 +489,8 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
 }
 
 // R(k): ring copy of chunk k (own bytes for C1 and stage 2, match_end - 2, literals; zero
-// past the block end), in the second half of step k - 3, so that C1(k - 1)'s ring read can
-// start a step later without waiting for anything
+// past the block end), at the start of step k - 2, right before C1(k - 1) reads chunks k - 1
+// and k from the ring (same wave: in order)
 template <bool FAST = false>
 __device__ __forceinline__ void prod_ring(EncLds &S, const Blk &B, int k, int lane,
                                           const uint32_t (&X)[2]) {
@@ -755,7 +757,7 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     O.q0 = W.q;
     O.Lf = O.iv.x & 0x7Fu;                               // forward match length
     // match_end - 2 (:680) of every lane's match, read from the ring now so that the
-    // second half's hash needs no LDS round trip (the ring holds chunks k - 12 .. k + 3,
+    // second half's hash needs no LDS round trip (the ring holds chunks k - 13 .. k + 2,
     // and a match the producer finished ends before p + 81; a match the walker extends
     // is hashed from the input instead)
     O.e2v = ring8(S, P + (uint32_t)lane + O.Lf - 2u);
@@ -1132,6 +1134,11 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             // In flight, oldest first: A(s+2), Y(s+1) x2, E(s) -> A(s+2) at 3.
             vm_wait<kWin ? 0 : 3>();
             STAT(9);   // (stats build: load waits)
+            // ring copy of chunk s+2 (loaded a step ago), then C1(s+1)'s own bytes (chunks
+            // s+1 and s+2) from the ring: one wave's LDS operations complete in order.  (Until
+            // round 3 chunk s+3 was copied in the second half of step s, which then waited
+            // for a load issued half a step earlier: -2.7 % encode time.)
+            prod_ring<F>(S, B, s + 2, lane, cur.X);
             uint32_t X6[6];   // C1(s+1)'s own bytes: in the ring since last step, read first
             prod_own(S, s + 1, lane, X6);
             prod_load<SMALL, F>(B, s + 3, lane, nxt.X);
@@ -1147,11 +1154,11 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             __syncthreads();
             STAT(6);
             prod_stage2_issue<SMALL, F>(S, B, s + 1, lane, nxt.q, nxt.E);
-            // E(s), A(s+3), Y(s+2) x2, E(s+1) -> E(s) and A(s+3) at 3
+            // E(s), A(s+3), Y(s+2) x2, E(s+1) -> E(s) at 4 (A(s+3), issued half a step ago,
+            // is not needed before the next step)
             STAT(7);
-            vm_wait<kWin ? 0 : 3>();
+            vm_wait<kWin ? 0 : 4>();
             STAT(9);
-            prod_ring<F>(S, B, s + 3, lane, nxt.X);
             prod_finish<SMALL, F>(S, B, s, lane, cur.q, cur.E);
             STAT(7);
             __syncthreads();
@@ -1255,7 +1262,8 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         if (E.pend == 0) {
             if (avail != 0u && (avail >= 48u || s - E.last >= APE_EMIT_EVERY)) {
                 // piece L runs in the second half of step s, when the ring holds input
-                // [64 (s - 12), 64 (s + 4)) (chunk s + 3 is being written over s - 13)
+                // [64 (s - 13), 64 (s + 3)) (chunk s + 2 was written over s - 14 at the
+                // start of step s; s + 3 overwrites s - 13 at the start of step s + 1)
                 emit_fetch(S, B, lane, E, avail, s >= 12 ? 64u * (uint32_t)(s - 12) : 0u);
                 E.last = s;
             }
