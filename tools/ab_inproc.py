@@ -5,7 +5,8 @@ Every variant (libapenetwork_amd/libape_lz4_amd_<v>.so, "base" = the product lib
 loaded into ONE process; the same device-resident App. C blocks are encoded and decoded by
 each variant in turn, ROUNDS times, timed with HIP events on one stream; prints the median
 encode / decode times and checks each variant's round trip (decode == input, and the
-encoded bytes decoded by the base library's decoder).
+encoded bytes decoded by the base library's decoder) and whether each variant's compressed bytes
+equal the first variant's (sizes of every block, bytes of 256 sampled blocks).
 usage: ab_inproc.py NBLOCKS ROUNDS v1 v2 ..."""
 import ctypes as C
 import os
@@ -52,13 +53,25 @@ def main():
 
     t = {v: ([], []) for v in names}
     ok = {}
+    ref = None   # the first variant's compressed bytes: the others are compared with them
     for v in names:   # warm-up + check
-        enc(libs[v]); dec(libs[v]); torch.cuda.synchronize()
+        enc(libs[v]); torch.cuda.synchronize()
+        same = None
+        if ref is None:
+            ref = (comp.clone(), csz.clone())
+        else:
+            same = bool(torch.equal(csz, ref[1])) and all(
+                bool(torch.equal(comp[i, :int(csz[i])], ref[0][i, :int(csz[i])]))
+                for i in range(0, nb, max(1, nb // 256)))
+        dec(libs[v]); torch.cuda.synchronize()
         ok[v] = bool((dres == n).all()) and bool(torch.equal(out, src))
         ratio = nb * n / int(csz.sum())
         dec(libs[names[0]]); torch.cuda.synchronize()
         ok[v] = ok[v] and bool((dres == n).all()) and bool(torch.equal(out, src))
-        print("%-12s ok %s ratio %.4f" % (v, ok[v], ratio), flush=True)
+        print("%-12s ok %s ratio %.4f%s" % (v, ok[v], ratio, "" if same is None else
+                                             "  bytes %s the first variant's (256 sampled blocks)"
+                                             % ("identical to" if same else "DIFFER from")),
+              flush=True)
     for r in range(rounds):
         for v in names:
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
