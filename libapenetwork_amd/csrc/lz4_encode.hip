@@ -121,10 +121,11 @@ constexpr uint32_t I_TRUNC = 1u << 7, I_HASHABLE = 1u << 13;
 static_assert(kEagerLen + kExt2 < 128u, "len fits 7 bits");
 
 struct __attribute__((aligned(16))) EncLds {
-    uint16_t tab[kHSize];
     // input byte x at ring byte (x mod kRingE); the first 64 bytes are mirrored
-    // after the end, so a 36-byte read never wraps (immediate LDS offsets)
+    // after the end, so a 36-byte read never wraps (immediate LDS offsets).  At LDS offset
+    // 0, so that a read's dwords share one address register (ds_read2 offsets)
     uint32_t ring[kRingE / 4 + 16];
+    uint16_t tab[kHSize];
     uint2 info[2][64];               // producer -> walker, chunk k in [k & 1]
     uint32_t scr[kScr];              // producer scratch: earliest lane per low hash bits
     uint2 q[kQ];                     // walker -> emitter: sequence records, record r in
@@ -260,7 +261,7 @@ __device__ __forceinline__ uint32_t hash5(uint32_t x1, uint32_t b4) {
     // (__umul24 returns int: do the sum and the shift unsigned)
     const uint32_t v = (uint32_t)__umul24(lo, 0x9E3779u) + (uint32_t)__umul24(hi, 0xC2B2AEu);
     if constexpr (kHSize == (1 << kHLog)) return v >> (32 - kHLog);
-    else return (uint32_t)__umul24(v >> 16, (uint32_t)kHSize) >> 16;
+    else return __umulhi(v, (uint32_t)kHSize);   // v scaled onto [0, kHSize): one v_mul_hi_u32
 }
 
 // v_ffbl_b32 / v_ffbh_u32: lowest / highest set bit, 0xFFFFFFFF for 0 (inline asm
