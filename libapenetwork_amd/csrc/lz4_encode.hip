@@ -126,7 +126,9 @@ struct __attribute__((aligned(16))) EncLds {
     // 0, so that a read's dwords share one address register (ds_read2 offsets)
     uint32_t ring[kRingE / 4 + 16];
     uint16_t tab[kHSize];
-    uint2 info[2][64];               // producer -> walker, chunk k in [k & 1]
+    uint2 info[64];                  // producer -> walker: chunk k, written in the second half of
+                                     // step k, read at the start of step k + 1 (before the
+                                     // producer writes chunk k + 1 after the mid barrier)
     uint32_t scr[kScr];              // producer scratch: earliest lane per low hash bits
     uint2 q[kQ];                     // walker -> emitter: sequence records, record r in
                                      // [r % kQ]: {lit | (match length - 4) << 16, offset}
@@ -650,7 +652,7 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
             trunc = mine == kExt2 && R.lim > R.base + kExt2;
         }
     }
-    S.info[k & 1][lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
+    S.info[lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
                                          (R.hashable ? I_HASHABLE : 0u),
                                      (R.has ? p - R.c : 0u) | (R.h << 16));
 }
@@ -754,7 +756,7 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     const uint32_t P = 64u * (uint32_t)k;
     O.walked = O.members = 0;
     O.m_back = O.m_len = O.an = 0;
-    O.iv = S.info[k & 1][lane];
+    O.iv = S.info[lane];
     O.q0 = W.q;
     O.Lf = O.iv.x & 0x7Fu;                               // forward match length
     // match_end - 2 (:680) of every lane's match, read from the ring now so that the
@@ -1111,7 +1113,7 @@ __device__ __forceinline__ void prefix_history(EncLds &S, const Blk &B, int lane
 // Three waves per block, one role each, in lock step (two barriers per step):
 //   step s, first half : producer A(s+3) B(s+2) C1(s+1) | walker walks s-1 | emitter writes
 //                                                         |   the pair (s-4, s-3) (every 2nd step)
-//   step s, second half: producer C2(s) -> info[s%3]     | walker inserts s-1, publishes
+//   step s, second half: producer C2(s) -> info     | walker inserts s-1, publishes
 //                                                         | emitter sizes s-2
 // Table inserts (second half) never overlap the producer's lookups (first half).
 template <bool SMALL, bool ACC>
