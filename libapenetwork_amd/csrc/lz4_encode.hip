@@ -10,8 +10,8 @@
 //
 // One 192-thread workgroup (three waves, one role each) per block; a batch holds
 // ~1M blocks, so most of the parallelism comes from many blocks in flight (9 per
-// CU).  Per block the LDS (17.4 KiB) holds a hash table like the reference's (:449-462:
-// u16 positions, a hash of 5 bytes; 6912 entries instead of 8192, see kHSize), a 1 KiB
+// CU).  Per block the LDS (17.5 KiB) holds a hash table like the reference's (:449-462:
+// u16 positions, a hash of 5 bytes; 7200 entries instead of 8192, see kHSize), a 1 KiB
 // ring of recent input and the hand-over records between the roles.  The input stays in
 // HBM/L2.
 //
@@ -66,12 +66,13 @@ namespace {
 #endif
 constexpr int kHLog = APE_LZ4_HLOG;
 // Table entries.  The reference's 8192 (2^13) entries make the block's LDS 20.4 KiB, so
-// 8 blocks fit a CU; 6912 entries (the 13-bit hash scaled onto [0, 6912)) make it 17.4 KiB,
-// inside the 17.5 KiB (35 x 512-byte LDS granules) that fits 9 blocks = 27 waves per CU
-// (7 per SIMD: <= 72 VGPRs).  Measured on 131072 blocks: encode -4.6 %, ratio 3.1464 ->
-// 3.1279 (tools/enc_model.c models the ratio per table size).
+// 8 blocks fit a CU; 7200 entries (the hash scaled onto [0, 7200)) make it 17.5 KiB (17904 B),
+// inside the 35 x 512-byte LDS granules that fit 9 blocks = 27 waves per CU (7 per SIMD:
+// <= 72 VGPRs).  Measured on 131072 blocks: 6912 entries -4.6 % encode time vs 8192, ratio
+// 3.1464 -> 3.1279; 7200 (once the info array was single-buffered) 3.1329 at the same time
+// (tools/enc_model.c models the ratio per table size).
 #ifndef APE_LZ4_TSIZE
-#define APE_LZ4_TSIZE 6912
+#define APE_LZ4_TSIZE 7200
 #endif
 constexpr int kHSize = APE_LZ4_TSIZE;
 static_assert(kHSize <= (1 << kHLog) && kHSize % 8 == 0, "table size");
