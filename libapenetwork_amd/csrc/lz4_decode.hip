@@ -397,17 +397,21 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const bool e_in = FASTD && (fin ? iend > (uint32_t)D.csize
                                     : (uint32_t)q > (uint32_t)D.csize);
     const bool e_cap = cpy + ml + (uint32_t)(kMinMatch + kLastLiterals) > ucap;   // :1444
-    const bool stop = fin || e_off || mlerr || e_cap || e_in;
-    const bool bad = fin ? (badfin || e_in) : stop;
+    // stop = fin || e_off || mlerr || e_cap || e_in; bad = fin ? badfin || e_in : stop
     const int rv = fin ? ((badfin || e_in) ? -ipl - 1 : (int)(FASTD ? iend : cpy))
                        : ((e_off || mlerr) ? -ipo - 1 : -q - 1);
-    const uint64_t sm = wave_ballot(mem && stop);
+    // (ballots of the single conditions, combined as wave masks: no per-lane 0/1)
+    const uint64_t fm = wave_ballot(fin);
+    const uint64_t stm = fm | wave_ballot(e_off) | wave_ballot(mlerr) | wave_ballot(e_cap) |
+                         wave_ballot(e_in);
+    const uint64_t badm = (fm & (wave_ballot(badfin) | wave_ballot(e_in))) | (~fm & stm);
+    const uint64_t sm = M & stm;
     uint64_t emit = M;
     int st = ST_MORE;
     if (sm) {
         const int T = __ffsll((long long)sm) - 1;
         res = (int)lane_val((uint32_t)rv, T);
-        const bool tbad = lane_val(bad ? 1u : 0u, T) != 0u;
+        const bool tbad = (badm >> T) & 1ull;
         // members before T (error) or up to T (final literals)
         emit = tbad ? ((1ull << T) - 1ull) : ((2ull << T) - 1ull);   // T <= 43
         st = tbad ? ST_ERR : ST_DONE;
@@ -613,20 +617,20 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
     const uint64_t need = (mpend && lane > 0 && k0 <= k1)
                               ? (((2ull << k1) - 1ull) & ~((1ull << k0) - 1ull)) : 0ull;
     uint64_t done = ~pm;
+    // lanes still pending = pm & ~done; kept as wave masks (a ballot of compares folds into
+    // the compares; a ballot of a combined bool made the compiler materialise a 0/1)
+    const uint64_t lpm = wave_ballot(lp);
     wave_sync();
     for (;;) {
         diag += 1u;
-        const bool go = mpend && lp && (need & ~done) == 0ull;
-        const uint64_t gm = wave_ballot(go);
+        const uint64_t gm = pm & ~done & lpm & wave_ballot((need & ~done) == 0ull);
         if (gm) {
-            lane_match<DICT>(L, D, base, go, ma, nm, off, glb);
-            mpend = mpend && !go;
+            lane_match<DICT>(L, D, base, lane_in(gm), ma, nm, off, glb);
             done |= gm;
         } else {   // the first pending sequence is a whole-wave item, and its sources are done
             const int f = __builtin_ctzll(pm & ~done);
             diag += 0x10000u;
             coop_match<DICT>(L, D, base, lane_val(ma, f), lane_val(nm, f), lane_val(off, f));
-            if (lane == f) mpend = false;
             done |= 1ull << f;
         }
         if (!(pm & ~done)) break;
