@@ -1357,7 +1357,11 @@ lz4_encode_kernel(BlockArgs a) {
     B.k0 = D / 64;
     // compress_fast's acceleration (:789-808) trades ratio for speed; here that is the
     // in-chunk candidate (-11 % encode time, ratio -1.7 % on App. C data)
+#ifdef APE_EXP_NOL
+    B.noL = true;   // diagnostic: no in-chunk candidate search (its LDS atomics)
+#else
     B.noL = ACC;
+#endif
     B.stride = ACC ? (a.accel < (1 << 20) ? (uint32_t)a.accel : 1u << 20) : 1u;
     B.pat = 0;
     if (ACC)
