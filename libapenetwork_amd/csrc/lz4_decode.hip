@@ -298,6 +298,9 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
 // (lanes [0, cnt)); X = the chain's exit (next token position >= 64, or kHopTerm after a
 // final / failing sequence, kHopCplx before a complex token); lastp = the last member.
 constexpr uint32_t kHopTerm = 0x80u, kHopCplx = 0xC0u;
+#ifndef APE_LZ4_DCHAIN16
+#define APE_LZ4_DCHAIN16 1
+#endif
 template <bool FASTD>
 __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, uint32_t &pos,
                                          int &cnt, uint32_t &X, uint32_t &lastp) {
@@ -315,7 +318,6 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
     const uint32_t J1 = jump(hop, hop);
     const uint32_t J2 = jump(J1, J1);
     const uint32_t J3 = jump(J2, J2);
-    const uint32_t J4 = jump(J3, J3);
     const uint32_t t = (uint32_t)D.lane;
     uint32_t p = (t & 1u) ? lane_val(hop, 0) : 0u;
     const uint32_t p2 = jump(J1, p);
@@ -324,8 +326,24 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
     p = (t & 4u) ? p4 : p;
     const uint32_t p8 = jump(J3, p);
     p = (t & 8u) ? p8 : p;
+#if APE_LZ4_DCHAIN16
+    // Lanes t < 16 are final now.  The chain has more than 15 members only when its member
+    // 15 exists (a 64-byte window averages ~14 sequences on App. C data); otherwise every
+    // lane t >= 15 holds the exit J^15(0) (exits absorb), and J^16 with its two dependent
+    // ds_bpermute rounds is skipped.
+    const uint32_t p15 = lane_val(p, 15);
+    if (p15 < 256u) {   // wave-uniform
+        const uint32_t J4 = jump(J3, J3);
+        const uint32_t p16 = jump(J4, p);
+        p = (t & 16u) ? p16 : p;
+    } else {
+        p = t >= 16u ? p15 : p;
+    }
+#else
+    const uint32_t J4 = jump(J3, J3);
     const uint32_t p16 = jump(J4, p);
     p = (t & 16u) ? p16 : p;
+#endif
     p >>= 2;
     pos = t < 32u ? p : kHopTerm;
     cnt = __popcll(wave_ballot(pos < 64u));
