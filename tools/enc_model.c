@@ -216,7 +216,7 @@ static long model3(const uint8_t *in, int n, int hlog, int R, int lag, int sb, i
 }
 
 
-/* Kernel policy (lz4_encode.hip / lz4_encode_v2.hip): fixed 64-position chunks; the table lags `lag`
+/* Kernel policy (lz4_encode.hip): fixed 64-position chunks; the table lags `lag`
  * chunks (walked positions + match_end - 2); L = earliest lane of the chunk with the
  * same low `sb` hash bits; catch-up <= 4.  pol 0: T and L measured in full, longer
  * wins (tie: closer); pol 7: L measured to 12 bytes only, taken when T is shorter
