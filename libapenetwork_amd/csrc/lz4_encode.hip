@@ -584,7 +584,10 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     // (bitwise on bools: lane masks combined by the scalar unit, no materialised 0/1)
     const bool okT = can & (cT < p) & (cT >= 4u) & (Y[1] == X[1]);
     const bool okL = can & (jL < (uint32_t)lane) & (cL != cT) & (Z[1] == X[1]);   // jL = ~0 if noL
-    R.lim = can ? B.mlimit - p : 0u;
+    // (FAST: the match limit lies >= 132 bytes past every lane, beyond anything C1 and C2
+    // measure, so it never cuts a length: no limit arithmetic at all)
+    R.lim = FAST ? 0xFFFFu : (can ? B.mlimit - p : 0u);   // (a FAST chunk finished by a
+                                                            // general step: no cut either)
     // measured unconditionally (selects, no branches): every lane reads Y, so the
     // compiler sees the candidate load consumed on every path.  T to 16 bytes, L to 12:
     // L (the closer one) is taken when T is shorter than 12 and L at least as long,
@@ -599,8 +602,12 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     R.base = pickL ? kEagerL : kEagerLen;
     // (two ballots of compares fold into the compares; a ballot of their AND made the
     // compiler materialise a 0/1 and compare it again)
-    R.tmask = wave_ballot(R.len >= R.base) & wave_ballot(R.lim > R.base);
-    R.len = umin(R.len, R.lim);
+    if (FAST) {
+        R.tmask = wave_ballot(R.len >= R.base);
+    } else {
+        R.tmask = wave_ballot(R.len >= R.base) & wave_ballot(R.lim > R.base);
+        R.len = umin(R.len, R.lim);
+    }
     R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
     R.has = okT | okL;
     R.h = h;
@@ -649,8 +656,8 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
             if (R.rank - first < kGroups) mine = m2;
         }
         if (lane_in(R.tmask)) {
-            len = umin(R.base + mine, R.lim);
-            trunc = mine == kExt2 && R.lim > R.base + kExt2;
+            len = FAST ? R.base + mine : umin(R.base + mine, R.lim);
+            trunc = mine == kExt2 && (FAST || R.lim > R.base + kExt2);
         }
     }
     S.info[lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
