@@ -466,8 +466,13 @@ template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_fetch_t(const Blk &B, int k, int lane, uint32_t cT,
                                              uint32_t (&Y)[6]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-    const bool tryT = (FAST || k < B.nch) && cT < p && cT >= 4u;
-    loadv<kYW>(B.in, B.un, tryT ? cT - 4u : 0u, Y, FAST || (!SMALL && 64 * k + 83 <= B.n));
+    if (FAST) {   // any address in [0, p): a lane whose T is not a candidate (C1 rechecks
+                  // cT < p and cT >= 4) loads harmless bytes -- min + saturating subtract
+        loadv<kYW>(B.in, B.un, __builtin_elementwise_sub_sat(umin(cT, p - 1u), 4u), Y, true);
+        return;
+    }
+    const bool tryT = k < B.nch && cT < p && cT >= 4u;
+    loadv<kYW>(B.in, B.un, tryT ? cT - 4u : 0u, Y, !SMALL && 64 * k + 83 <= B.n);
 }
 
 // B(k): hash, table + in-chunk candidates, T fetch issue
@@ -660,8 +665,10 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
             trunc = mine == kExt2 && (FAST || R.lim > R.base + kExt2);
         }
     }
+    // (FAST: the chunk lies inside the block, every lane hashable -- also the prologue's
+    // chunk when the first step is FAST)
     S.info[lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
-                                         (R.hashable ? I_HASHABLE : 0u),
+                                  ((FAST || R.hashable) ? I_HASHABLE : 0u),
                                      (R.has ? p - R.c : 0u) | (R.h << 16));
 }
 
