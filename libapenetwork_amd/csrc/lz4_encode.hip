@@ -588,7 +588,9 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     for (int t = 0; t < 4; t++) Z[t] = bperm(X[t], jL);
     // (bitwise on bools: lane masks combined by the scalar unit, no materialised 0/1)
     const bool okT = can & (cT < p) & (cT >= 4u) & (Y[1] == X[1]);
-    const bool okL = can & (jL < (uint32_t)lane) & (cL != cT) & (Z[1] == X[1]);   // jL = ~0 if noL
+    // (no cL != cT test: when L's candidate is T's, L is kept only when T < 12 bytes, and then
+    // both give the same position, length and preceding bytes)
+    const bool okL = can & (jL < (uint32_t)lane) & (Z[1] == X[1]);   // jL = ~0 if noL
     // (FAST: the match limit lies >= 132 bytes past every lane, beyond anything C1 and C2
     // measure, so it never cuts a length: no limit arithmetic at all)
     R.lim = FAST ? 0xFFFFu : (can ? B.mlimit - p : 0u);   // (a FAST chunk finished by a
