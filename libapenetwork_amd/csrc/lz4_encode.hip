@@ -61,6 +61,11 @@ hipError_t enc_stats_read(unsigned long long *out, int reset) {
 
 namespace {
 
+#ifdef APE_EXP_CNT_NTR   // diagnostic: counters only, no phase timers
+#undef STAT
+#define STAT(i) do {} while (0)
+#endif
+
 #ifndef APE_LZ4_HLOG
 #define APE_LZ4_HLOG 13
 #endif
@@ -91,6 +96,11 @@ constexpr uint32_t kEagerL = 12;     // ... for the in-chunk candidate L
 // per candidate, 16 candidates per pass (a second pass is rare).
 constexpr uint32_t kExt2 = 64;
 constexpr uint32_t kGroups = 16;
+// Stage 2 only for the last lane of each run of truncated lanes with the same offset and base
+// (the others' lengths follow from it, exactly: DESIGN.md 3.1)
+#ifndef APE_LZ4_S2RUN
+#define APE_LZ4_S2RUN 1
+#endif
 #ifndef APE_LZ4_ERING
 #define APE_LZ4_ERING 1024
 #endif
@@ -430,6 +440,7 @@ struct Part {                        // C1 result of one chunk, finished by C2
     bool has, hashable;
     uint64_t tmask;                  // lanes whose candidate reached its measured length (a
                                      // wave mask: no per-lane 0/1 to materialise)
+    uint64_t smask;                  // ... of them, the lanes stage 2 measures
 };
 
 // One parity of the producer pipeline (the step loop is unrolled by two, so no
@@ -538,7 +549,7 @@ __device__ __forceinline__ void prod_own(const EncLds &S, int k, int lane, uint3
 __device__ __forceinline__ bool stage2_group(const Part &R, int lane, uint32_t first, uint32_t p,
                                              uint32_t &cb, uint32_t &eo) {
     const uint32_t r = R.rank - first, i16 = 16u * ((uint32_t)lane & 3u);
-    const bool push = lane_in(R.tmask) && r < kGroups;
+    const bool push = lane_in(R.smask) && r < kGroups;
     const int tgt = (int)((push ? 4u * r : ((uint32_t)lane | 1u)) << 2);
     cb = dpp<0x00>(0u, (uint32_t)__builtin_amdgcn_ds_permute(tgt, (int)(R.c + R.base))) + i16;
     eo = dpp<0x00>(0u, (uint32_t)__builtin_amdgcn_ds_permute(tgt, (int)(p + R.base))) + i16;
@@ -555,7 +566,11 @@ __device__ __forceinline__ uint32_t stage2_len(const EncLds &S, int lane, uint32
                                                128u * ((uint32_t)lane & 3u));
     d = umin(d, dpp<0xB1>(0u, d));   // quad_perm [1,0,3,2]
     d = umin(d, dpp<0x4E>(0u, d));   // quad_perm [2,3,0,1]
+#if APE_LZ4_S2RUN   // continuation point + length: a run member subtracts its own
+    return eo + umin(d >> 3, kExt2);
+#else
     return umin(d >> 3, kExt2);
+#endif
 }
 
 // C1(k): verify / measure to kEagerLen bytes / pick; queue the truncated candidates and issue
@@ -615,6 +630,17 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
         R.tmask = wave_ballot(R.len >= R.base) & wave_ballot(R.lim > R.base);
         R.len = umin(R.len, R.lim);
     }
+#if APE_LZ4_S2RUN
+    {   // lane i + 1 truncated with the same offset and base: in[p, p+1) == in[c, c+1), so the
+        // match from p is one byte longer than lane i + 1's (and lim one larger): only the
+        // run's last lane is measured
+        const uint32_t key = (R.c - (uint32_t)lane) + (R.base << 24);
+        const uint32_t keyn = dpp<kDppWaveShl1>(0u, key);   // lane 63: 0, never a key
+        R.smask = R.tmask & ~((R.tmask >> 1) & wave_ballot(key == keyn));
+    }
+#else
+    R.smask = R.tmask;
+#endif
     R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
     R.has = okT | okL;
     R.h = h;
@@ -627,7 +653,7 @@ template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_stage2_issue(const EncLds &S, const Blk &B, int k, int lane,
                                                   Part &R, uint32_t (&E)[4]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-    const uint64_t tb = R.tmask;
+    const uint64_t tb = R.smask;   // (a run member's rank is its run's last lane's)
     R.ntr = (uint32_t)__popcll(tb);
     R.rank = lane_rank(tb);
     uint32_t cb;
@@ -663,6 +689,9 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
             if (R.rank - first < kGroups) mine = m2;
         }
         if (lane_in(R.tmask)) {
+#if APE_LZ4_S2RUN
+            mine = umin(mine - (p + R.base), kExt2);   // + distance to the run's last lane
+#endif
             len = FAST ? R.base + mine : umin(R.base + mine, R.lim);
             trunc = mine == kExt2 && (FAST || R.lim > R.base + kExt2);
         }
@@ -1174,6 +1203,19 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             __syncthreads();
             STAT(6);
             prod_stage2_issue<SMALL, F>(S, B, s + 1, lane, nxt.q, nxt.E);
+#ifdef APE_EXP_CNT_NTR
+            if (s + 1 < B.nch) {   // diagnostic: stage-2 queue sizes and same-offset runs
+                const uint32_t ntr = nxt.q.ntr;
+                const uint32_t off = 64u * (uint32_t)(s + 1) + (uint32_t)lane - nxt.q.c;
+                const uint32_t offn = bperm(off, (uint32_t)lane + 1u);
+                const uint64_t tm = nxt.q.tmask;
+                const bool tn = lane < 63 && ((tm >> (lane + 1)) & 1ull);
+                const uint64_t der = wave_ballot(lane_in(tm) && tn && offn == off);
+                const uint32_t roots = ntr - (uint32_t)__popcll(der);
+                STAT_ADD(0, ntr); STAT_ADD(1, ntr > 16u); STAT_ADD(2, ntr > 32u); STAT_ADD(3, ntr > 48u);
+                STAT_ADD(4, 1); STAT_ADD(5, roots); STAT_ADD(6, roots > 16u); STAT_ADD(7, roots > 32u);
+            }
+#endif
             // E(s), A(s+3), Y(s+2) x2, E(s+1) -> E(s) at 4 (A(s+3), issued half a step ago,
             // is not needed before the next step)
             STAT(7);
@@ -1248,7 +1290,9 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             STAT(4);
             walk_finish<ACC>(B, s - 1, lane, W, O);
             walk_publish(S, B, s - 1, lane, O, qn);
+#ifndef APE_EXP_CNT_NTR
             STAT_ADD(11, __popcll(O.members));
+#endif
             STAT(1);
             STAT_ADD(10, 3);
             __syncthreads();

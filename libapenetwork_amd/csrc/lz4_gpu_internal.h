@@ -62,7 +62,7 @@ __device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t v) {
 }
 constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114,
               kDppRowShr8 = 0x118, kDppBcast15 = 0x142, kDppBcast31 = 0x143,
-              kDppWaveShr1 = 0x138;
+              kDppWaveShr1 = 0x138, kDppWaveShl1 = 0x130;
 
 // Inclusive scans over the 64 lanes (Hillis-Steele inside 16-lane rows, then
 // row broadcasts) -- VALU latency instead of LDS-crossbar shuffles.
