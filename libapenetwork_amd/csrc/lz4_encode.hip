@@ -689,11 +689,14 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
             if (R.rank - first < kGroups) mine = m2;
         }
         if (lane_in(R.tmask)) {
-#if APE_LZ4_S2RUN
-            mine = umin(mine - (p + R.base), kExt2);   // + distance to the run's last lane
-#endif
+#if APE_LZ4_S2RUN   // mine - p = the run's last lane's length + the distance to it
+            const uint32_t cap = R.base + kExt2, full = mine - p;
+            len = FAST ? umin(full, cap) : umin(umin(full, cap), R.lim);
+            trunc = full >= cap && (FAST || R.lim > cap);
+#else
             len = FAST ? R.base + mine : umin(R.base + mine, R.lim);
             trunc = mine == kExt2 && (FAST || R.lim > R.base + kExt2);
+#endif
         }
     }
     // (FAST: the chunk lies inside the block, every lane hashable -- also the prologue's
