@@ -149,8 +149,10 @@ def test_pathological_runs(cuda, product, oracle):
 
 def _boundary_copies(n, seed, lens):
     """Random bytes, then back-copies whose lengths sit on the encoder's measurement edges
-    (C1 measures T to 20 bytes and L to 12, stage 2 adds 64: lengths 11-13, 19-21, 75-77,
-    83-86), each followed by one random byte so the match ends exactly there."""
+    (C1 measures T to 16 bytes and L to 12, stage 2 adds 64: lengths 11-13, 15-17, 75-77,
+    79-81; and the edges of the round-2 20-byte T: 19-21, 83-86), each followed by one random
+    byte so the match ends exactly there.  Inside such a copy consecutive lanes share the
+    offset: stage 2 measures the run's last lane and the others derive their lengths."""
     rng = random.Random(seed)
     out = bytearray(rng.randbytes(2048))
     while len(out) < n:
@@ -166,9 +168,10 @@ def test_stage2_measurement_edges(cuda, product, oracle):
     """Matches ending exactly at the producer's measured lengths (C1's 12/20 bytes, stage 2's
     +64) and chunks where more than 16 lanes are truncated (a second stage-2 pass): valid
     output, and the ratio close to the reference's on the same data."""
-    lens = [11, 12, 13, 19, 20, 21, 75, 76, 77, 83, 84, 85, 86]
+    lens = [11, 12, 13, 15, 16, 17, 19, 20, 21, 75, 76, 77, 79, 80, 81, 83, 84, 85, 86]
     srcs = [_boundary_copies(65536, s, lens) for s in range(16)] + \
-           [_boundary_copies(65536, 100 + s, [83, 84, 85, 86, 150, 300]) for s in range(8)] + \
+           [_boundary_copies(65536, 100 + s, [79, 80, 81, 83, 84, 85, 86, 150, 300])
+            for s in range(8)] + \
            [_boundary_copies(n, 200 + n, lens) for n in (150, 300, 1000, 4099, 65535)]
     rs, comps = run_encode(cuda, product, srcs)
     for s, r, c in zip(srcs, rs, comps):
