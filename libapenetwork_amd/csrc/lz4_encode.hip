@@ -1217,6 +1217,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
                 const uint32_t roots = ntr - (uint32_t)__popcll(der);
                 STAT_ADD(0, ntr); STAT_ADD(1, ntr > 16u); STAT_ADD(2, ntr > 32u); STAT_ADD(3, ntr > 48u);
                 STAT_ADD(4, 1); STAT_ADD(5, roots); STAT_ADD(6, roots > 16u); STAT_ADD(7, roots > 32u);
+                STAT_ADD(8, roots > 8u); STAT_ADD(9, (uint32_t)__popcll(nxt.q.smask)); // (= roots)
             }
 #endif
             // E(s), A(s+3), Y(s+2) x2, E(s+1) -> E(s) at 4 (A(s+3), issued half a step ago,
@@ -1295,6 +1296,9 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             walk_publish(S, B, s - 1, lane, O, qn);
 #ifndef APE_EXP_CNT_NTR
             STAT_ADD(11, __popcll(O.members));
+#else   // members the walker extends (their match reached C1 + stage 2's measured length)
+            STAT_ADD(11, __popcll(O.members & wave_ballot((O.iv.x & I_TRUNC) != 0u)));
+            STAT_ADD(12, __popcll(O.members));
 #endif
             STAT(1);
             STAT_ADD(10, 3);
