@@ -84,8 +84,11 @@ static_assert(kHSize <= (1 << kHLog) && kHSize % 8 == 0, "table size");
 #ifndef APE_LZ4_WAVES_PER_EU
 #define APE_LZ4_WAVES_PER_EU 7
 #endif
+// T measured to 12 bytes (as L): with stage 2 finishing only the runs' last lanes, the extra
+// truncated lanes cost less than C1's fifth dword (the 16-byte C1 of rounds 2-3 measured +1.5 %;
+// same decisions -- L is taken only when T < 12 -- so the same bytes; both bases 12)
 #ifndef APE_LZ4_EAGER_T
-#define APE_LZ4_EAGER_T 16
+#define APE_LZ4_EAGER_T 12
 #endif
 constexpr uint32_t kEagerLen = APE_LZ4_EAGER_T;   // match bytes measured by C1 (T candidate)
 static_assert(kEagerLen == 12 || kEagerLen == 16 || kEagerLen == 20, "C1 measures T to 12, 16 or 20 bytes");
