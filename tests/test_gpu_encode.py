@@ -149,8 +149,8 @@ def test_pathological_runs(cuda, product, oracle):
 
 def _boundary_copies(n, seed, lens):
     """Random bytes, then back-copies whose lengths sit on the encoder's measurement edges
-    (C1 measures T to 16 bytes and L to 12, stage 2 adds 64: lengths 11-13, 15-17, 75-77,
-    79-81; and the edges of the round-2 20-byte T: 19-21, 83-86), each followed by one random
+    (C1 measures T and L to 12 bytes, stage 2 adds 64: lengths 11-13, 75-77; and the edges of
+    the earlier 16- and 20-byte T: 15-17, 19-21, 79-81, 83-86), each followed by one random
     byte so the match ends exactly there.  Inside such a copy consecutive lanes share the
     offset: stage 2 measures the run's last lane and the others derive their lengths."""
     rng = random.Random(seed)
