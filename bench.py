@@ -761,16 +761,15 @@ def _free_port():
 def launch_ranks(args):
     """`--gpus N` without a launcher: start N ranks of this script (one process per GPU,
     RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set) and exit with their status.
-    Nothing here touches a GPU (torch.cuda.device_count() does not initialise HIP on this
-    image), so the children start from a clean process.  Rank 0's stdout is this process's
-    stdout (the one JSON line); the other ranks' stdout goes to stderr."""
+    Nothing here loads torch or the HIP runtime: the devices are counted from the KFD
+    topology in sysfs (sharding.visible_gpu_count), so the children start from a process
+    that never touched a GPU (tests/test_multigpu.py checks this).  Rank 0's stdout is this
+    process's stdout (the one JSON line); the other ranks' stdout goes to stderr."""
     import signal
 
-    import torch
-
-    from libapenetwork_amd.sharding import launch_plan
+    from libapenetwork_amd.sharding import launch_plan, visible_gpu_count
     try:
-        plan = launch_plan(args.gpus, args.blocks, torch.cuda.device_count(),
+        plan = launch_plan(args.gpus, args.blocks, visible_gpu_count(),
                            os.environ.get("APE_BENCH_DEVICE"), args.weak, _free_port())
     except ValueError as e:
         log("bench.py: %s (set APE_BENCH_DEVICE=<id> to rehearse N ranks on one device)" % e)
@@ -929,9 +928,15 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    # poison every output of the step before the timed region, so the verification below
+    # can only pass on bytes, sizes and results that the timed steps themselves produced
+    comp.fill_(0xA5)
+    out.fill_(0x5A)
+    csz.fill_(-1)
+    dres.fill_(-7)
     torch.cuda.synchronize()
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    evs =[[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -1014,8 +1019,13 @@ def main():
                      "basis": "sum(n + c) x 2 (R+W) / step time, all ranks, vs 8 TB/s x GPUs"}}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        # after every rank's timed region (the gather above is a rendezvous), so at N > 1 the
+        # reference's host run competes with no rank's GPU work; the other ranks only exit
         cpu = cpu_baseline(n, kind, args.cpu_blocks)
+        if cpu is not None and world > 1:
+            cpu["note"] = ("timed by rank 0 after every rank's timed steps (the other %d "
+                           "ranks are exiting)" % (world - 1))
     c2 = None
     if rank == 0 and world == 1 and not args.no_config2:
         del src, comp, out

@@ -5,10 +5,13 @@
  * Same 35 declared entry points, same argument meaning, same return
  * conventions, same ABI-visible struct sizes (APE_LZ4_stream_t = 16416 B,
  * APE_LZ4_streamDecode_t = 32 B), so ape_socket.c / ape_buffer.c and any
- * embedder link against libape_lz4_amd.so unchanged.  In this implementation the
- * one-shot block codec (compress_default / compress_fast* / decompress_safe /
- * decompress_safe_partial) runs as CDNA4 HIP kernels on an MI355X; see
- * ape_lz4_gpu.h for the batched device API that is the performance path.
+ * embedder link against libape_lz4_amd.so unchanged (tests/c/ape_socket_caller.c is
+ * such a caller, built with -Wall -Werror by the CPU suite).  One-shot calls run the
+ * library's host codec by default -- byte-identical to the reference, at its speed on one
+ * core -- and move to CDNA4 HIP kernels on an MI355X only when the caller opts in
+ * (APE_LZ4_gpu_set_oneshot_host_below / APE_LZ4_ONESHOT_HOST_BELOW; a single block never
+ * beats one host core on the GPU).  ape_lz4_gpu.h is the batched
+ * device API, the performance path.
  *
  * Reference citations are file:line into the reference tree.
  */

@@ -117,10 +117,18 @@ constexpr bool kWin = kRingE >= 65536u;
 #endif
 constexpr uint32_t kScr = 1u << APE_LZ4_SCRBITS;  // in-chunk candidate scratch entries
 constexpr int kSmall = 128;          // smaller blocks take the byte-load path
-// Sequence records in flight between the walker and the emitter: the emitter takes 64 at
-// a time, fewer than 64 + 16 (a chunk has <= 16 matches) are ever queued, so a batch
-// being read and the walker's next records never share a slot.
+// Sequence records in flight between the walker and the emitter.  The emitter reads up to
+// 64 records into registers at a fetch (its slots are free from then on); it fetches when
+// kFetchAt are queued or every APE_EMIT_EVERY steps, and while a batch is pending it
+// finishes that batch at once (emit_all, no fetch) when kEmitAll are queued.  The walker adds
+// at most kChunkRecs per step (a match covers >= 4 of the chunk's 64 positions).  Worst
+// case: kEmitAll - 1 queued at a pending step, + kChunkRecs before emit_all, + kChunkRecs
+// before the next fetch -- that must fit the ring, or the walker overwrites unread records.
 constexpr uint32_t kQ = 128;
+constexpr uint32_t kFetchAt = 48, kEmitAll = 80, kChunkRecs = 64u / 4u;
+static_assert((kQ & (kQ - 1u)) == 0u, "record ring indexed by & (kQ - 1)");
+static_assert(kEmitAll - 1u + 2u * kChunkRecs <= kQ, "walker -> emitter record ring overflow");
+static_assert(kFetchAt < kEmitAll, "a fetch precedes emit_all");
 #ifndef APE_EMIT_EVERY
 #define APE_EMIT_EVERY 8             // emitter: a batch every this many steps (at most)
 #endif
@@ -1334,14 +1342,14 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         // S.qn: the walker's count as of its last publish (before the previous barrier)
         const uint32_t avail = (uint32_t)__builtin_amdgcn_readfirstlane(S.qn) - E.qc;
         if (E.pend == 0) {
-            if (avail != 0u && (avail >= 48u || s - E.last >= APE_EMIT_EVERY)) {
+            if (avail != 0u && (avail >= kFetchAt || s - E.last >= APE_EMIT_EVERY)) {
                 // piece L runs in the second half of step s, when the ring holds input
                 // [64 (s - 13), 64 (s + 3)) (chunk s + 2 was written over s - 14 at the
                 // start of step s; s + 3 overwrites s - 13 at the start of step s + 1)
                 emit_fetch(S, B, lane, E, avail, s >= 12 ? 64u * (uint32_t)(s - 12) : 0u);
                 E.last = s;
             }
-        } else if (avail >= 80u) {   // rare: never on App. C data
+        } else if (avail >= kEmitAll) {   // rare: never on App. C data
             emit_all(S, B, lane, E);
         } else {
             emit_step(S, B, lane, E);

@@ -260,8 +260,6 @@ BlockArgs ptr_args(const char *const *src, const int *in, char *const *dst, cons
 
 }  // namespace
 
-// the device probe already ran and found a device (never triggers the probe itself)
-
 extern "C" {
 
 int APE_LZ4_gpu_init(void) { return check_device(); }

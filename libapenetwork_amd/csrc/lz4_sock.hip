@@ -436,8 +436,13 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
         parsed = 0;
     }
     sock_add(7, now_ns() - trx);
-    for (int i = 0; i < 2; i++) {   // the last batches' stage times
-        if (rc == 0 && busy[i] && hipStreamSynchronize(d[i].st) == hipSuccess) {
+    for (int i = 0; i < 2; i++) {   // drain every batch in flight, whatever rc is
+        if (!busy[i]) continue;
+        if (hipStreamSynchronize(d[i].st) != hipSuccess) {
+            if (rc == 0) rc = APE_LZ4_GPU_ELAUNCH;   // its results never reached h_result
+            continue;
+        }
+        if (rc == 0) {   // the last batches' results and stage times
             sock_add(10, ev_ns(d[i].tev[0], d[i].tev[1]));
             sock_add(11, ev_ns(d[i].tev[1], d[i].tev[2]));
             sock_add(12, ev_ns(d[i].tev[2], d[i].tev[3]));

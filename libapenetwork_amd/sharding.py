@@ -10,6 +10,7 @@ There is no collective on the data path and no RCCL at all: the only cross-rank
 operations are the benchmark's barrier, the max-over-ranks step time and the gather of
 per-rank scalars, all on host scalars over a gloo (CPU) process group.
 """
+import os
 
 
 def shard_strong(rank, world, total_blocks):
@@ -21,16 +22,63 @@ def shard_strong(rank, world, total_blocks):
     return first, (rank + 1) * total_blocks // world - first
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _visible(n, spec):
+    """Devices left of `n` after a *_VISIBLE_DEVICES list (indices or UUIDs); the runtime
+    stops at the first index that does not exist, and an empty list hides every device."""
+    if spec is None:
+        return n
+    k = 0
+    for tok in (t.strip() for t in spec.split(",")):
+        if not tok:
+            break
+        if tok.isdigit() and int(tok) >= n:
+            break
+        k += 1
+    return min(k, n)
+
+
+def visible_gpu_count(nodes=None, environ=None):
+    """GPUs this process would see, counted WITHOUT the HIP runtime: the KFD topology nodes
+    with SIMDs (CPU nodes have none), then ROCR_VISIBLE_DEVICES, HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES and GPU_DEVICE_ORDINAL applied in the runtime's order.  bench.py's
+    launcher calls this in the parent, which must not initialise a GPU before it starts the
+    ranks (torch.cuda.device_count() may fall back to hipGetDeviceCount).  None when the
+    topology is not readable but /dev/kfd exists (the ranks then check for their device
+    themselves); 0 without /dev/kfd."""
+    env = os.environ if environ is None else environ
+    nodes = KFD_NODES if nodes is None else nodes
+    try:
+        names = os.listdir(nodes)
+    except OSError:
+        return None if os.path.exists("/dev/kfd") else 0
+    n = 0
+    for name in names:
+        try:
+            with open(os.path.join(nodes, name, "properties")) as f:
+                props = dict(line.split(None, 1) for line in f if len(line.split()) == 2)
+        except (OSError, ValueError):
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    n = _visible(n, env.get("ROCR_VISIBLE_DEVICES"))
+    n = _visible(n, env.get("HIP_VISIBLE_DEVICES", env.get("CUDA_VISIBLE_DEVICES")))
+    return _visible(n, env.get("GPU_DEVICE_ORDINAL"))
+
+
 def launch_plan(ngpus, total_blocks, device_count, rehearsal_device=None, weak=False,
                 master_port=29500):
     """The ranks `bench.py --gpus N` starts by itself (one process per GPU):
     a list of {rank, device, first_block, nblocks, env} with the RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_* environment of each child.  Raises ValueError when fewer than N
     devices are visible, unless `rehearsal_device` (APE_BENCH_DEVICE) puts every rank on
-    that one device."""
+    that one device.  device_count None (not known without the runtime) starts the ranks
+    and leaves the check to them."""
     if ngpus < 1:
         raise ValueError("--gpus must be >= 1, got %r" % (ngpus,))
-    if rehearsal_device is None and device_count < ngpus:
+    if rehearsal_device is None and device_count is not None and device_count < ngpus:
         raise ValueError("--gpus %d but only %d device(s) visible" % (ngpus, device_count))
     plan = []
     for r in range(ngpus):

@@ -367,8 +367,10 @@ void cpu_bench_free(void *h)
  *     decompress_safe_continue into an 8 KiB block, append it to the 64 KiB dictionary
  *     buffer (memmove when full, :1398-1413) and setStreamDecode on it (:1421).
  * One TX and one RX thread per connection; messages are the App. C blocks of
- * `msg` bytes (the benchmark's 64 KiB).  out: [0] seconds, [1] payload bytes,
- * [2] wire bytes, [3] errors.
+ * `msg` bytes (the benchmark's 64 KiB).  Timed region = the GPU leg's (bench.py sock_leg):
+ * every message is generated before the clock starts and the delivered payload is compared
+ * after it stops, so the clock holds only compress/frame/write and read/parse/decode/ring
+ * work.  out: [0] seconds, [1] payload bytes, [2] wire bytes, [3] errors.
  * --------------------------------------------------------------------------------- */
 #include <arpa/inet.h>
 #include <netinet/in.h>
@@ -395,6 +397,9 @@ typedef struct {
     int fd_tx, fd_rx, msg, nmsg, kind, conn;
     long long wire;
     int bad;
+    uint8_t *src;   /* nmsg * msg bytes, generated before the clock starts */
+    uint8_t *dst;   /* nmsg * msg bytes, the delivered payload, compared after it stops */
+    long long delivered;
 } sconn_t;
 
 static int sk_write_all(int fd, const char *p, size_t n)
@@ -408,16 +413,17 @@ static int sk_write_all(int fd, const char *p, size_t n)
     return 0;
 }
 
+/* TX: compress + frame + write only (the messages are generated before
+ * the clock, as the GPU leg's are) */
 static void *sk_tx(void *arg)
 {
     sconn_t *c = (sconn_t *)arg;
     const int cap = SK_BLOCK + SK_BLOCK / 255 + 16;
-    uint8_t *msg = malloc((size_t)c->msg);
     char *frames = malloc((size_t)(c->msg / SK_BLOCK + 1) * (cap + 4));
     char *dict = malloc(SK_DICT);
     void *st = c->mk();
     for (int m = 0; m < c->nmsg && st; m++) {
-        synth_blocks(msg, c->msg, c->msg, (long long)c->conn * c->nmsg + m, 1, c->kind);
+        const uint8_t *msg = c->src + (size_t)m * c->msg;
         int pos = 0;
         for (int off = 0; off < c->msg; off += SK_BLOCK) {
             const int len = c->msg - off < SK_BLOCK ? c->msg - off : SK_BLOCK;
@@ -432,23 +438,24 @@ static void *sk_tx(void *arg)
     }
     shutdown(c->fd_tx, SHUT_WR);
     if (st) c->fr(st);
-    free(msg); free(frames); free(dict);
+    free(frames); free(dict);
     return NULL;
 }
 
+/* RX: read + parse + decode + dictionary ring, each decoded block delivered to the
+ * connection's payload buffer (the application's callback, :1423); compared after the clock */
 static void *sk_rx(void *arg)
 {
     sconn_t *c = (sconn_t *)arg;
     const int cap = SK_BLOCK + SK_BLOCK / 255 + 16;
     const size_t bsz = 1u << 20;
+    const long long total = (long long)c->nmsg * c->msg;
     char *buf = malloc(bsz);
     char *dict = malloc(SK_DICT);
     char tmp[SK_BLOCK];
-    uint8_t *expect = malloc((size_t)c->msg);
     void *sd = c->mkd();
     size_t used = 0;
-    int dpos = 0, m = 0, mpos = 0;
-    synth_blocks(expect, c->msg, c->msg, (long long)c->conn * c->nmsg, 1, c->kind);
+    int dpos = 0;
     for (;;) {
         ssize_t r = read(c->fd_rx, buf + used, bsz - used);
         if (r < 0) { c->bad++; break; }
@@ -471,12 +478,9 @@ static void *sk_rx(void *arg)
                 dpos += rc;
             }
             c->setd(sd, dict, dpos);
-            if (m < c->nmsg && memcmp(tmp, expect + mpos, (size_t)rc) != 0) c->bad++;
-            mpos += rc;
-            if (mpos == c->msg && ++m < c->nmsg) {
-                mpos = 0;
-                synth_blocks(expect, c->msg, c->msg, (long long)c->conn * c->nmsg + m, 1, c->kind);
-            }
+            if (c->delivered + rc > total) { c->bad++; goto done; }
+            memcpy(c->dst + c->delivered, tmp, (size_t)rc);
+            c->delivered += rc;
             p += 4 + (size_t)sz;
         }
         memmove(buf, buf + p, used - p);
@@ -484,9 +488,8 @@ static void *sk_rx(void *arg)
         if (r == 0) break;
     }
 done:
-    if (m != c->nmsg) c->bad++;
     if (sd) c->frd(sd);
-    free(buf); free(dict); free(expect);
+    free(buf); free(dict);
     return NULL;
 }
 
@@ -517,6 +520,10 @@ int cpu_sock_run(const char *lib, const char *prefix, int nconn, int msg, int nm
     for (int i = 0; i < nconn && rc == 0; i++) {
         cs[i] = base;
         cs[i].msg = msg; cs[i].nmsg = nmsg; cs[i].kind = kind; cs[i].conn = i;
+        cs[i].src = malloc((size_t)nmsg * msg + 1);
+        cs[i].dst = malloc((size_t)nmsg * msg + 1);
+        if (!cs[i].src || !cs[i].dst) { rc = -4; break; }
+        synth_blocks(cs[i].src, msg, msg, (long long)i * nmsg, nmsg, kind);
         int ls = socket(AF_INET, SOCK_STREAM, 0), one = 1;
         struct sockaddr_in a;
         socklen_t al = sizeof a;
@@ -550,8 +557,13 @@ int cpu_sock_run(const char *lib, const char *prefix, int nconn, int msg, int nm
     }
     const double t1 = now_s();
     for (int i = 0; i < nconn; i++) {
+        if (rc == 0 && (cs[i].delivered != (long long)nmsg * msg ||
+                        memcmp(cs[i].dst, cs[i].src, (size_t)nmsg * msg) != 0))
+            bad++;
         if (cs[i].fd_tx > 0) close(cs[i].fd_tx);
         if (cs[i].fd_rx > 0) close(cs[i].fd_rx);
+        free(cs[i].src);
+        free(cs[i].dst);
     }
     free(cs); free(th);
     if (rc) return rc;

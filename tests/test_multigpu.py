@@ -161,6 +161,75 @@ def test_launch_plan_for_gpus_flag():
     assert [p["nblocks"] for p in plan] == [65536, 65536]
 
 
+def _fake_topology(root, gpus, cpus=1):
+    """A KFD topology tree like /sys/class/kfd/kfd/topology/nodes: CPU nodes have no SIMDs."""
+    for i in range(cpus + gpus):
+        d = os.path.join(root, str(i))
+        os.makedirs(d)
+        simd = 0 if i < cpus else 256
+        with open(os.path.join(d, "properties"), "w") as f:
+            f.write("cpu_cores_count %d\nsimd_count %d\ngfx_target_version %d\n" % (
+                64 if i < cpus else 0, simd, 0 if i < cpus else 90500))
+    return root
+
+
+def test_visible_gpu_count_without_runtime(tmp_path):
+    """The launcher's device count comes from sysfs, with the runtime's visibility lists."""
+    from libapenetwork_amd.sharding import visible_gpu_count
+    nodes = _fake_topology(str(tmp_path / "nodes"), gpus=8, cpus=2)
+    assert visible_gpu_count(nodes, {}) == 8
+    assert visible_gpu_count(nodes, {"HIP_VISIBLE_DEVICES": "0,3"}) == 2
+    assert visible_gpu_count(nodes, {"CUDA_VISIBLE_DEVICES": "5"}) == 1
+    assert visible_gpu_count(nodes, {"ROCR_VISIBLE_DEVICES": "1,2,3,4",
+                                     "HIP_VISIBLE_DEVICES": "0,1,7"}) == 2   # 7 >= 4 stops
+    assert visible_gpu_count(nodes, {"HIP_VISIBLE_DEVICES": ""}) == 0
+    assert visible_gpu_count(nodes, {"GPU_DEVICE_ORDINAL": "2,9"}) == 1
+
+
+_LAUNCHER_PROBE = r"""
+import json, os, subprocess, sys
+sys.path.insert(0, sys.argv[1])
+import bench
+from libapenetwork_amd import sharding
+sharding.KFD_NODES = sys.argv[2]
+started = []
+class FakeProc:
+    def __init__(self, cmd, env=None, stdout=None):
+        started.append({k: env[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")})
+        self.pid = 0
+    def poll(self):
+        return 0
+subprocess.Popen = FakeProc
+import argparse
+rc = bench.launch_ranks(argparse.Namespace(gpus=8, blocks=1 << 20, weak=False))
+maps = open("/proc/self/maps").read()
+print(json.dumps({"rc": rc, "started": started, "torch": "torch" in sys.modules,
+                  "hip": ("libamdhip64" in maps) or ("libhsa-runtime" in maps)}))
+"""
+
+
+def test_launcher_touches_no_gpu_runtime(tmp_path):
+    """`bench.py --gpus 8`'s parent counts devices from sysfs and starts the ranks without
+    importing torch or mapping the HIP/HSA runtime: the children begin
+    in a process tree where nothing initialised a GPU."""
+    import json
+    import subprocess
+    import sys
+    nodes = _fake_topology(str(tmp_path / "nodes"), gpus=8)
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "APE_BENCH_DEVICE", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+              "ROCR_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", _LAUNCHER_PROBE, ROOT, nodes], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["rc"] == 0 and not res["torch"] and not res["hip"]
+    assert [s["RANK"] for s in res["started"]] == [str(i) for i in range(8)]
+    assert all(s["WORLD_SIZE"] == "8" and s["MASTER_ADDR"] == "127.0.0.1"
+               for s in res["started"])
+
+
 def _bench(args, env_extra):
     import subprocess
     import sys

@@ -129,7 +129,7 @@ def test_socket_loopback_roundtrip(cuda, product, kind, batch):
     nb, n = 40, 65536
     src = _blocks(cuda, product, nb, n, kind)
     dst = _dst(nb, n)
-    res = np.zeros(nb, dtype=np.int32)
+    res = np.full(nb, -9, dtype=np.int32)        # every entry must be written, last batch too
     tx, rx = _pair()
     out = {}
 
@@ -220,3 +220,24 @@ def test_socket_recv_malformed_stream(cuda, product, damage):
     tx.close()
     rx.close()
     assert (dst[:, n:] == 0xCB).all()
+
+
+def test_cpu_sock_baseline_times_codec_only(oracle):
+    """bench.py config5.cpu_baseline harness (oracle/cpu_bench.c cpu_sock_run): the
+    reference's chained socket codec over loopback delivers every payload byte intact, over
+    one and several connections.  Its messages are generated before the clock and compared
+    after it; the payload count and wire bytes are returned."""
+    import ctypes as C
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = C.CDLL(os.path.join(root, "oracle", "libcpubench.so"))
+    lib.cpu_sock_run.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.POINTER(C.c_double)]
+    ref = os.path.join(root, "oracle", "_ref", "libape_lz4_ref.so")
+    path, prefix = (ref, b"APE_LZ4_") if os.path.exists(ref) else (
+        os.path.join(root, "oracle", "liblz4_oracle.so"), b"orc_")
+    out = (C.c_double * 4)()
+    for nconn, msg, nmsg, kind in ((1, 65536, 16, 1), (3, 20000, 5, 1), (2, 65536, 4, 0)):
+        assert lib.cpu_sock_run(path.encode(), prefix, nconn, msg, nmsg, kind, out) == 0
+        assert out[3] == 0 and out[1] == nconn * msg * nmsg and out[0] > 0
+        assert out[2] > 4 * nconn * nmsg * ((msg + 8191) // 8192)
