@@ -636,6 +636,145 @@ def sock_leg(args):
     return line
 
 
+def sock_chained_leg(args):
+    """The reference wire format through the GPU over many sockets (VERDICT r3
+    item 6): M loopback TCP connections, each a chained stream exactly as ape_socket writes it
+    (64 KiB messages in 8 KiB chunks, each compressed against the stream's previous <= 64 KiB,
+    [int32 size][block] frames; ref src/ape_socket.c:811-871) and reads it (decompress against
+    the last 64 KiB, :1333-1467).  TX thread: APE_LZ4_chain_send -- per round one message per
+    connection, all chunks in one withPrefix launch, frames written to each socket.  RX (this
+    thread): APE_LZ4_chain_recv -- poll + split-safe parser per connection, per round nch
+    usingDict launches of M blocks.  Every byte is compared.  Beside it: the reference's own
+    socket codec on the same number of connections (oracle/cpu_bench.c cpu_sock_run)."""
+    import socket
+    import threading
+
+    import torch
+
+    import libapenetwork_amd as amd
+
+    torch.cuda.set_device(0)
+    if amd.gpu_init() != 0:
+        raise SystemExit("GPU codec unavailable: %s" % amd.gpu_last_error())
+    M, nmsg, n = args.chain_conns, args.chain_msgs, 65536
+    h_msgs = torch.empty((nmsg, M, n), dtype=torch.uint8, pin_memory=True)
+    h_out = torch.zeros((nmsg, M, n), dtype=torch.uint8, pin_memory=True)
+    g = torch.empty((M, n), dtype=torch.uint8, device="cuda")
+    for m in range(nmsg):   # App. C gen_comp, connection i's message m = block m * M + i (untimed)
+        amd.synth_blocks(g, n, m * M, 1)
+        h_msgs[m].copy_(g)
+    torch.cuda.synchronize()
+    del g
+    msgs, out = h_msgs.numpy(), h_out.numpy()
+    status = np.zeros(M, dtype=np.int32)
+
+    def pairs():
+        ps = []
+        for _ in range(M):
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.bind(("127.0.0.1", 0))
+            srv.listen(1)
+            t = socket.create_connection(srv.getsockname())
+            r, _ = srv.accept()
+            srv.close()
+            for s_ in (t, r):
+                s_.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
+                s_.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
+            ps.append((t, r))
+        return ps
+
+    def run(k):
+        ps = pairs()
+        tx, rx = amd.Chain(M, n), amd.Chain(M, n)
+        res = {}
+
+        def txf():
+            try:
+                res["wire"] = tx.send([t.fileno() for t, _ in ps], msgs[:k])
+            except Exception as e:
+                res["err"] = e
+            finally:
+                for t, _ in ps:
+                    t.shutdown(socket.SHUT_WR)
+
+        t0 = time.perf_counter()
+        th = threading.Thread(target=txf)
+        th.start()
+        got = rx.recv([r.fileno() for _, r in ps], out[:k], status)
+        th.join()
+        wall = time.perf_counter() - t0
+        for t, r in ps:
+            t.close()
+            r.close()
+        tx.free()
+        rx.free()
+        if "err" in res:
+            raise res["err"]
+        return wall, got, res["wire"]
+
+    run(min(nmsg, 2))               # warm-up
+    h_out.zero_()
+    amd.socket_stats(reset=True)
+    wall, got, wire = run(nmsg)
+    split = amd.socket_stats(reset=True)
+    ok = got == nmsg * M * n and bool((status == 0).all()) and bool(torch.equal(h_out, h_msgs))
+    payload = nmsg * M * n
+    cpu = None
+    if not args.no_cpu_baseline:
+        lib = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
+        lib.cpu_sock_run.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.POINTER(C.c_double)]
+        ref = os.path.join(ROOT, "oracle", "_ref", "libape_lz4_ref.so")
+        path, prefix, kind = ((ref, b"APE_LZ4_", "reference") if os.path.exists(ref) else
+                              (os.path.join(ROOT, "oracle", "liblz4_oracle.so"), b"orc_", "port"))
+        o = (C.c_double * 4)()
+        cm = min(M, 128)
+        cmsg = max(8, args.chain_cpu_bytes // (cm * n))
+        usable, cores = host_cores()
+        if lib.cpu_sock_run(path.encode(), prefix, cm, n, cmsg, 1, o) == 0 and o[3] == 0:
+            cpu = {"value": round(o[1] / o[0] / GIB, 3), "unit": "GiB/s", "cores": usable,
+                   "kind": kind, "connections": cm, "threads": 2 * cm,
+                   "wire_GBps": round(o[2] / o[0] / 1e9, 3), "seconds": round(o[0], 2),
+                   "sample": "%d connections x %d x 64 KiB App. C messages, the reference socket "
+                             "codec (compress_fast_continue + saveDict / decompress_safe_continue "
+                             "+ 64 KiB ring), one TX and one RX thread per connection on %d usable "
+                             "cores; generated before and compared after the clock" % (cm, cmsg, usable),
+                   "host": cores}
+    ceiling = None
+    try:
+        cb = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
+        cb.sock_ceiling.argtypes = [C.c_longlong, C.c_int, C.POINTER(C.c_double)]
+        o2 = (C.c_double * 2)()
+        if cb.sock_ceiling(int(wire), 4 << 20, o2) == 0:
+            ceiling = round(o2[1] / o2[0] / 1e9, 3)
+    except OSError:
+        pass
+    return {
+        "metric": "LZ4 GiB/s, the reference socket wire format (chained 8 KiB blocks) through the "
+                  "GPU over %d loopback TCP connections" % M,
+        "value": round(payload / wall / GIB, 3), "unit": "GiB/s", "n_gpus": 1,
+        "higher_is_better": True, "dtype": "u8",
+        "data": "synthetic (SURVEY App. C gen_comp), one 64 KiB message per connection per round",
+        "config": {"workload": "%d connections x %d x 64 KiB messages = %.2f GiB, 8 KiB chained "
+                               "chunks, [int32 size][block] frames" % (M, nmsg, payload / GIB)},
+        "wall_s": round(wall, 3), "wire_bytes": int(wire), "ratio": round(payload / (wire - 4 * nmsg * M * 8), 4),
+        "wire_GBps": round(wire / wall / 1e9, 3), "verified": ok,
+        "ceiling_GBps": ceiling,
+        "ceiling": "plain bytes over one 127.0.0.1 TCP connection, 4 MiB write()s (sock_ceiling), "
+                   "same wire bytes",
+        "split_ms": {k: v for k, v in split.items() if k in (
+            "tx_write_ms", "tx_gpu_wait_ms", "tx_batches", "tx_total_ms", "rx_total_ms",
+            "rx_read_ms", "rx_parse_ms", "rx_gpu_wait_ms", "rx_batches")},
+        "split_note": "rx_read_ms = poll + read() until every connection holds a round; "
+                      "rx_parse_ms = payload staging; rx_gpu_wait_ms = waiting on round m - 2",
+        "cpu_baseline": cpu,
+    }
+
+
+def sock_chained_bench(args):
+    print(json.dumps(sock_chained_leg(args)), flush=True)
+
+
 def cpu_sock_baseline(n):
     """The reference's own socket codec over loopback TCP on this host's cores (BASELINE
     config 5; oracle/cpu_bench.c cpu_sock_run: ape_socket.c's TX -- 8 KiB blocks with
@@ -836,11 +975,20 @@ def main():
     ap.add_argument("--sock-blocks", type=int, default=1 << 17,
                     help="config 5 sample (131072 x 64 KiB = 8 GiB)")
     ap.add_argument("--sock-batch", type=int, default=2048)
+    ap.add_argument("--sock-chained", action="store_true",
+                    help="the reference wire format (chained 8 KiB blocks) over many sockets")
+    ap.add_argument("--chain-conns", type=int, default=128)
+    ap.add_argument("--chain-msgs", type=int, default=128,
+                    help="64 KiB messages per connection (128 x 128 x 64 KiB = 1 GiB)")
+    ap.add_argument("--chain-cpu-bytes", type=int, default=1 << 30,
+                    help="payload of the reference socket-codec baseline run")
     args = ap.parse_args()
     if args.e2e:
         return e2e_bench(args)
     if args.sock:
         return sock_bench(args)
+    if args.sock_chained:
+        return sock_chained_bench(args)
     if args.stream:
         return stream_bench(args)
     if args.rand4k:

@@ -222,6 +222,33 @@ long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_strid
 long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int block_size,
                                      int nblocks, int batch, int *h_result);
 
+/* ---- chained socket streams: the reference wire format through the GPU (lz4_sock.hip) ----
+ * nconn connections, each a stream exactly as the reference socket writes and reads it:
+ * every message cut into 8 KiB chunks, each compressed against the previous <= 64 KiB of
+ * its stream and framed [int32 size][block] (ref src/ape_socket.c:811-871); the receiver
+ * decodes each frame against the previous 64 KiB it decoded (:1333-1467).  An unmodified
+ * reference peer reads what chain_send writes and writes what chain_recv reads.
+ *   chain_new(nconn, msg_len) : device history windows for nconn send and nconn receive
+ *                        streams, msg_len bytes per message (NULL on failure)
+ *   chain_send         : nmsg rounds; round m compresses message m of every connection
+ *                        (at h_msgs + (m * nconn + i) * msg_stride) in one GPU launch (a
+ *                        chunk's history is plaintext the sender has) and writes connection
+ *                        i's frames to fds[i].  Returns the bytes written or APE_LZ4_GPU_E*.
+ *   chain_recv         : nmsg rounds; reads every fd (poll), parses each connection's frames
+ *                        split-safe, decodes round m's message of every connection with one
+ *                        usingDict launch per 8 KiB chunk (the connections are the batch) into
+ *                        h_out + (m * nconn + i) * out_stride.  h_status[i] = 0 or the first
+ *                        bad result of connection i.  Returns the payload bytes or
+ *                        APE_LZ4_GPU_E* (EINVAL: malformed frame, early EOF, failed decode).
+ * One thread may send while another receives on the same chain. */
+typedef struct APE_LZ4_chain APE_LZ4_chain;
+APE_LZ4_chain *APE_LZ4_chain_new(int nconn, int msg_len);
+void APE_LZ4_chain_free(APE_LZ4_chain *c);
+long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msgs,
+                             size_t msg_stride, int nmsg);
+long long APE_LZ4_chain_recv(APE_LZ4_chain *c, const int *fds, char *h_out, size_t out_stride,
+                             int nmsg, int *h_status);
+
 /* Time split of the socket calls since the last reset, out[16] in ms: TX [0] H2D, [1] encode
  * + frame offsets + pack (GPU), [2] D2H, [3] write(), [4] host waiting for the GPU, [5]
  * batches (count), [6] the whole send call; RX [7] the whole receive loop, [8] read(), [9]

@@ -22,6 +22,7 @@ __all__ = [
     "decompress_fast_ptr_batch", "compress_destSize_ptr_batch", "RxBuf",
     "compress_destSize_scratch_ptr_batch", "destSize_scratch_size",
     "socket_send_blocks", "socket_recv_blocks", "socket_stats", "set_oneshot_host_below",
+    "Chain",
     "oneshot_on_gpu",
     "ONESHOT_HOST_ALL",
 ]
@@ -91,6 +92,10 @@ def lib():
             "APE_LZ4_socket_send_blocks": (ll, [i, p, sz, i, i, i]),
             "APE_LZ4_socket_recv_blocks": (ll, [i, p, sz, i, i, i, p]),
             "APE_LZ4_socket_stats": (i, [p, i]),
+            "APE_LZ4_chain_new": (p, [i, i]),
+            "APE_LZ4_chain_free": (None, [p]),
+            "APE_LZ4_chain_send": (ll, [p, p, p, sz, i]),
+            "APE_LZ4_chain_recv": (ll, [p, p, p, sz, i, p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -392,6 +397,54 @@ def socket_recv_blocks(fd, dst, block_size, batch, results):
     if r < 0:
         raise GpuError("APE_LZ4_socket_recv_blocks failed (%d): %s" % (r, gpu_last_error()))
     return r
+
+
+class Chain:
+    """APE_LZ4_chain: nconn chained socket streams in the reference wire format (8 KiB
+    chunks against the stream's last 64 KiB, [int32 size][block] frames; ref
+    src/ape_socket.c:811-871, :1333-1467) with the GPU codec batched across connections."""
+
+    def __init__(self, nconn, msg_len):
+        self.nconn, self.msg_len = int(nconn), int(msg_len)
+        self._c = lib().APE_LZ4_chain_new(self.nconn, self.msg_len)
+        if not self._c:
+            raise GpuError("APE_LZ4_chain_new failed: %s" % gpu_last_error())
+
+    def _fds(self, fds):
+        if len(fds) != self.nconn:
+            raise ValueError("need %d fds" % self.nconn)
+        return (_C.c_int * self.nconn)(*fds)
+
+    def send(self, fds, msgs):
+        """msgs: uint8 numpy [nmsg, nconn, S >= msg_len] (round m, connection i).  Returns the
+        bytes written."""
+        nmsg = int(msgs.shape[0])
+        r = lib().APE_LZ4_chain_send(self._c, self._fds(fds), _C.c_void_p(msgs.ctypes.data),
+                                     int(msgs.strides[1]), nmsg)
+        if r < 0:
+            raise GpuError("APE_LZ4_chain_send failed (%d): %s" % (r, gpu_last_error()))
+        return r
+
+    def recv(self, fds, out, status):
+        """out: uint8 numpy [nmsg, nconn, S >= msg_len]; status: int32 numpy [nconn].  Returns
+        the payload bytes (raises on a malformed stream or a failed decode)."""
+        nmsg = int(out.shape[0])
+        r = lib().APE_LZ4_chain_recv(self._c, self._fds(fds), _C.c_void_p(out.ctypes.data),
+                                     int(out.strides[1]), nmsg, _C.c_void_p(status.ctypes.data))
+        if r < 0:
+            raise GpuError("APE_LZ4_chain_recv failed (%d): %s" % (r, gpu_last_error()))
+        return r
+
+    def free(self):
+        if self._c:
+            lib().APE_LZ4_chain_free(self._c)
+            self._c = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 SOCKET_STATS = {"tx_h2d_ms": 0, "tx_encode_ms": 1, "tx_d2h_ms": 2, "tx_write_ms": 3,

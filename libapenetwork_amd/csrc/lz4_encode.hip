@@ -129,6 +129,9 @@ constexpr uint32_t kFetchAt = 48, kEmitAll = 80, kChunkRecs = 64u / 4u;
 static_assert((kQ & (kQ - 1u)) == 0u, "record ring indexed by & (kQ - 1)");
 static_assert(kEmitAll - 1u + 2u * kChunkRecs <= kQ, "walker -> emitter record ring overflow");
 static_assert(kFetchAt < kEmitAll, "a fetch precedes emit_all");
+#ifndef APE_LZ4_ACC_L
+#define APE_LZ4_ACC_L 0              // acceleration > 1 keeps the in-chunk candidate
+#endif
 #ifndef APE_EMIT_EVERY
 #define APE_EMIT_EVERY 8             // emitter: a batch every this many steps (at most)
 #endif
@@ -440,8 +443,7 @@ struct Blk {
                                      // history prefix (withPrefix encode), only hashed
     uint32_t nr;                     // bytes to encode (n - 64 k0)
     bool noL;                        // acceleration > 1: no in-chunk candidate
-    uint32_t stride;                 // acceleration: search every stride-th position
-    uint64_t pat;                    // bits 0, stride, 2 stride, ... (< 64)
+    uint32_t stride;                 // acceleration (compress_fast): the first search step
 };
 
 // ---------------- producer ----------------
@@ -720,9 +722,40 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
 // ---------------- walker ----------------
 struct Walk {
     uint32_t q;          // walk position (the next probe)
-    uint32_t anchor;     // start of the pending literals
-    uint32_t dense;      // acceleration: consecutive probes left before the stride phase
+    uint32_t anchor;     // start of the pending literals (= the last match end)
 };
+
+// compress_fast's search pattern (ref :591-600, :710-720): after a match end e the
+// reference tests e, searches from e + 1 with step 1 once, then takes the j-th step
+// searchMatchNb >> skipTrigger = acc + ((j - 1) >> 6): probes e, e+1, e+2, then
+// y = e + 2 + {acc, 2 acc, .., 64 acc, 64 acc + (acc+1), ..} -- regime r (gap acc + r) starts
+// after S_r = 64 (acc r + r (r - 1) / 2).  `Probe` is the regime of the chunk's first lane
+// relative to a far origin e0 (a chunk spans at most two regimes: each covers >= 128 positions
+// when acc >= 2); lanes whose origin is a match end inside the chunk are in regime 0.
+struct Probe {
+    uint32_t s0, s1, g0;   // S_r, S_{r+1}, acc + r
+};
+__device__ __forceinline__ Probe probe_regime(uint32_t P, uint32_t e0, uint32_t acc) {
+    const uint32_t y0 = P > e0 + 2u ? P - e0 - 2u : 0u;   // wave-uniform
+    uint32_t s = 0, g = acc;
+    while (y0 > s + 64u * g) {   // (scalar; a few trips per chunk at most)
+        s += 64u * g;
+        g++;
+    }
+    Probe R;
+    R.s0 = s;
+    R.s1 = s + 64u * g;
+    R.g0 = g;
+    return R;
+}
+// is position e + d probed?  far: e is the regime's origin e0; else d < 64 (regime 0)
+__device__ __forceinline__ bool probed(uint32_t d, bool far, const Probe &R, uint32_t acc) {
+    const uint32_t y = d - 2u;
+    const bool hi = far && y > R.s1;
+    const uint32_t base = far ? (hi ? R.s1 : R.s0) : 0u;
+    const uint32_t g = far ? (hi ? R.g0 + 1u : R.g0) : acc;
+    return d <= 2u || (y - base) % g == 0u;
+}
 
 // forward extension of the match at m (candidate cm) from L bytes on, with the
 // whole wave, 1 KiB per step; returns the full length (<= mlimit - m)
@@ -849,26 +882,17 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
         W.q = P + rel;
         return;
     }
+    // acceleration: a member is taken only at a probe position (probe_regime): from the last
+    // match end before the chunk (far), then from each member's end (near)
+    const Probe R = probe_regime(P, W.anchor, B.stride);
+    uint32_t e = W.anchor;
+    bool far = true;
     for (;;) {
-        // acceleration (:591-600): after a match end e the reference tests e (:710-720),
-        // then searches from e+1 with step 1 once and then step = acceleration (without
-        // the growth after 64 misses): probes e, e+1, e+2, e+2+a, e+2+2a, ...  `dense`
-        // = consecutive probes left from rel; then every stride-th.
-        const uint32_t dn = W.dense;
-        const uint64_t pm = !ACC ? ~0ull
-                                 : (dn ? ((1ull << dn) - 1ull) | (B.pat << (dn - 1u)) : B.pat);
-        const uint64_t w = (Hm >> rel) & pm;
-        if (w == 0) {   // next probe position past the chunk
-            if (!ACC) {
-                rel = 64u;
-            } else if (rel + dn > 64u) {          // still in the consecutive probes
-                W.dense = rel + dn - 64u;
-                rel = 64u;
-            } else {
-                const uint32_t b = dn ? rel + dn - 1u : rel;   // the stride phase's base
-                rel = b + ((64u - b + B.stride - 1u) / B.stride) * B.stride;
-                W.dense = 0;
-            }
+        const uint32_t x = P + (uint32_t)lane;
+        const uint64_t pm = wave_ballot(x >= e && probed(x - e, far, R, B.stride));
+        const uint64_t w = (Hm & pm) >> rel;
+        if (w == 0) {   // no probe with a match left in the chunk
+            rel = 64u;
             break;
         }
         const uint32_t j = rel + (uint32_t)__builtin_ctzll(w);
@@ -883,7 +907,8 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
         } else {
             rel = j + h;
         }
-        if (ACC) W.dense = 3u;   // a new search from the match end
+        e = P + rel;
+        far = false;
         if (rel >= 64u) break;
     }
     O.members = M;
@@ -912,7 +937,10 @@ __device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk 
     // walked = every position from the walk start that no match of this chunk covers
     // (with acceleration: the probed ones, every stride-th from the last match end)
     bool w = p >= umax(O.q0, pm);
-    if (ACC) w = w && (p - pm < 3u || (p - pm - 2u) % B.stride == 0u);
+    if (ACC) {   // the probed ones (the origin: the last match end before the lane)
+        const Probe R = probe_regime(P, anchor0, B.stride);
+        w = w && probed(p - pm, pm == anchor0, R, B.stride);
+    }
     O.walked = wave_ballot(w);
     W.anchor = umax(anchor0, lane_val(imax, 63));
 }
@@ -1283,7 +1311,6 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         uint32_t qn = 0;
         W.q = 64u * (uint32_t)k0;
         W.anchor = W.q;
-        W.dense = 3u;   // the first search probes 0, 1, 2, then every stride-th
         WalkOut O;
         __syncthreads();
         // chunk s - 1 is walked during step s for s in [k0 + 1, nch]; the first step and
@@ -1438,12 +1465,9 @@ lz4_encode_kernel(BlockArgs a) {
 #ifdef APE_EXP_NOL
     B.noL = true;   // diagnostic: no in-chunk candidate search (its LDS atomics)
 #else
-    B.noL = ACC;
+    B.noL = ACC && !APE_LZ4_ACC_L;
 #endif
     B.stride = ACC ? (a.accel < (1 << 20) ? (uint32_t)a.accel : 1u << 20) : 1u;
-    B.pat = 0;
-    if (ACC)
-        for (uint32_t i = 0; i < 64u; i += B.stride) B.pat |= 1ull << i;
     B.cap = (uint32_t)icap;
     B.un = (uint32_t)B.n;
     B.mstart = B.un >= 12 ? B.un - 12 : 0;   // matches start at <= n-12 (:585)

@@ -23,6 +23,8 @@
 //     next.  The event loop is not rebuilt: these are blocking calls for one connection
 //     (a caller runs TX and RX on their own threads, as the loopback benchmark does).
 #include <errno.h>
+#include <poll.h>
+#include <vector>
 #include <time.h>
 #include <atomic>
 #include <stdio.h>
@@ -457,6 +459,412 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
     }
     return rc ? rc : done;
 }
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------
+// Chained streams: the reference wire format through the GPU.
+//
+// The reference socket sends every message cut into 8 KiB chunks (APE_LZ4_BLOCK_SIZE,
+// src/ape_socket.c:39), each compressed with compress_fast_continue against the previous
+// <= 64 KiB of the connection's stream and framed [int32 size][block] (:811-871; saveDict
+// after the message keeps the history, :856); the receiver decodes each frame with
+// decompress_safe_continue against its 64 KiB dictionary buffer (:1386-1421).  A server holds
+// many connections, so the GPU batches them:
+//   TX: one message per connection per round.  A chunk's history is plaintext the sender
+//       already has, so all chunks of the round (nconn x nch) are compressed in ONE
+//       withPrefix launch, each against the bytes before it in its connection's device
+//       window; frames are packed on the GPU and written to each connection's socket.
+//   RX: per connection a receive buffer with the split-safe parser; a round takes one
+//       message (nch frames) from every connection and decodes it with nch usingDict
+//       launches of nconn blocks each (chunk k + 1's dictionary is chunk k's output, so
+//       the chunks of one stream are sequential; the connections are the batch).
+// Both sides keep a window of W bytes per connection on the device; when the next message
+// would pass its end, the last 64 KiB move to its start (one 2-D device copy for all).
+// Bytes on the wire: exactly the reference's format, so an unmodified reference peer reads
+// what chain_send writes and writes what chain_recv reads (tests/test_sock.py).
+namespace {
+
+constexpr int kChunk = 8192;                      // APE_LZ4_BLOCK_SIZE (:39)
+constexpr int kChunkBound = kChunk + kChunk / 255 + 16;   // APE_LZ4_COMPRESSBOUND(8192)
+constexpr size_t kChunkSlot = (kChunkBound + 15) & ~15;
+constexpr int kHist = 65536;                      // the dictionary (:43)
+
+// TX pointer arrays of a round: chunk t = (connection i, chunk j), t = i * nch + j
+__global__ void chain_tx_setup(char *win, size_t W, uint32_t pos, int msg, int nch, int n,
+                               char *slots, const char **src, int *size, int *pre, char **dst,
+                               int *cap) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int i = t / nch, j = t - i * nch;
+    const int len = msg - kChunk * j < kChunk ? msg - kChunk * j : kChunk;
+    src[t] = win + (size_t)i * W + pos + (size_t)kChunk * j;
+    size[t] = len;
+    pre[t] = (int)pos + kChunk * j;   // the whole stream so far (the encoder keeps what fits)
+    dst[t] = slots + (size_t)t * kChunkSlot;
+    cap[t] = len + len / 255 + 16;
+}
+
+// RX pointer arrays of a round, chunk-major (launch k decodes entries [k * nconn, (k+1) * nconn)):
+// entry k * nconn + i = chunk k of connection i, payload at stage + poff[i * nch + k]
+__global__ void chain_rx_setup(const char *stage, const long long *poff, char *win, size_t W,
+                               uint32_t pos, int msg, int nch, int nconn, const char **src,
+                               char **dst, int *cap, const char **dict, int *dsz) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nch * nconn) return;
+    const int k = e / nconn, i = e - k * nconn;
+    const uint32_t at = pos + (uint32_t)(kChunk * k);
+    const uint32_t h = at < (uint32_t)kHist ? at : (uint32_t)kHist;
+    src[e] = stage + poff[i * nch + k];
+    dst[e] = win + (size_t)i * W + at;
+    cap[e] = msg - kChunk * k < kChunk ? msg - kChunk * k : kChunk;
+    dict[e] = win + (size_t)i * W + at - h;
+    dsz[e] = (int)h;
+}
+
+}  // namespace
+
+struct APE_LZ4_chain {
+    int dev = 0, nconn = 0, msg = 0, nch = 0, nt = 0;
+    size_t W = 0;
+    // TX (one thread): device window, compressed slots, frames, pointer arrays
+    hipStream_t tst = nullptr;
+    hipEvent_t tev[2] = {nullptr, nullptr};
+    char *txwin = nullptr, *slots = nullptr, *frames = nullptr;
+    int *csz = nullptr, *size = nullptr, *pre = nullptr, *cap = nullptr;
+    const char **src = nullptr;
+    char **dst = nullptr;
+    long long *off = nullptr;
+    void *scratch = nullptr;
+    char *h_frames = nullptr;
+    long long *h_off[2] = {nullptr, nullptr};
+    uint32_t txpos = 0;
+    // RX (one thread): device window, staged payloads, pointer arrays, results
+    hipStream_t rst = nullptr;
+    hipEvent_t rev[2] = {nullptr, nullptr};
+    char *rxwin = nullptr, *rstage[2] = {nullptr, nullptr};
+    long long *rpoff[2] = {nullptr, nullptr};
+    int *rcsz[2] = {nullptr, nullptr}, *rcap = nullptr, *rdsz = nullptr, *rres[2] = {nullptr, nullptr};
+    const char **rsrc = nullptr, **rdict = nullptr;
+    char **rdst = nullptr;
+    char *h_stage[2] = {nullptr, nullptr};
+    long long *h_poff[2] = {nullptr, nullptr};
+    int *h_csz[2] = {nullptr, nullptr}, *h_res[2] = {nullptr, nullptr};
+    uint32_t rxpos = 0;
+};
+
+namespace {
+
+void chain_release(APE_LZ4_chain *c) {
+    if (c->tst) (void)hipStreamSynchronize(c->tst);
+    if (c->rst) (void)hipStreamSynchronize(c->rst);
+    for (void *p : {(void *)c->txwin, (void *)c->slots, (void *)c->frames, (void *)c->csz,
+                    (void *)c->size, (void *)c->pre, (void *)c->cap, (void *)c->src, (void *)c->dst,
+                    (void *)c->off, c->scratch, (void *)c->rxwin, (void *)c->rstage[0],
+                    (void *)c->rstage[1], (void *)c->rpoff[0], (void *)c->rpoff[1],
+                    (void *)c->rcsz[0], (void *)c->rcsz[1], (void *)c->rcap, (void *)c->rdsz,
+                    (void *)c->rres[0], (void *)c->rres[1], (void *)c->rsrc, (void *)c->rdict,
+                    (void *)c->rdst})
+        if (p) (void)hipFree(p);
+    for (void *p : {(void *)c->h_frames, (void *)c->h_off[0], (void *)c->h_off[1],
+                    (void *)c->h_stage[0], (void *)c->h_stage[1], (void *)c->h_poff[0],
+                    (void *)c->h_poff[1], (void *)c->h_csz[0], (void *)c->h_csz[1],
+                    (void *)c->h_res[0], (void *)c->h_res[1]})
+        if (p) (void)hipHostFree(p);
+    for (hipEvent_t e : {c->tev[0], c->tev[1], c->rev[0], c->rev[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (c->tst) (void)hipStreamDestroy(c->tst);
+    if (c->rst) (void)hipStreamDestroy(c->rst);
+    delete c;
+}
+
+template <typename T>
+bool dalloc(T *&p, size_t n) { return hipMalloc((void **)&p, n * sizeof(T)) == hipSuccess; }
+template <typename T>
+bool halloc(T *&p, size_t n) {
+    return hipHostMalloc((void **)&p, n * sizeof(T), hipHostMallocDefault) == hipSuccess;
+}
+
+// the window slides when the next message would pass its end: the last <= 64 KiB of every
+// connection's stream move to the start of its row (a 2-D device copy; rows never overlap
+// their source since W >= 2 x 64 KiB + msg)
+hipError_t chain_slide(char *win, size_t W, int nconn, uint32_t &pos, int msg, hipStream_t st) {
+    if ((size_t)pos + (size_t)msg <= W) return hipSuccess;
+    const uint32_t keep = pos < (uint32_t)kHist ? pos : (uint32_t)kHist;
+    const hipError_t e = hipMemcpy2DAsync(win, W, win + (pos - keep), W, keep, (size_t)nconn,
+                                          hipMemcpyDeviceToDevice, st);
+    pos = keep;
+    return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+APE_LZ4_chain *APE_LZ4_chain_new(int nconn, int msg_len) {
+    if (nconn <= 0 || msg_len <= 0 || msg_len > (1 << 24) || APE_LZ4_gpu_init() != 0) return nullptr;
+    APE_LZ4_chain *c = new APE_LZ4_chain();
+    (void)hipGetDevice(&c->dev);
+    c->nconn = nconn;
+    c->msg = msg_len;
+    c->nch = (msg_len + kChunk - 1) / kChunk;
+    c->nt = nconn * c->nch;
+    c->W = ((size_t)2 * kHist + (size_t)msg_len + 255) & ~(size_t)255;
+    const size_t nt = (size_t)c->nt, fr = nt * (kChunkSlot + 4) + 64;
+    bool ok = hipStreamCreateWithFlags(&c->tst, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->rst, hipStreamNonBlocking) == hipSuccess;
+    for (int b = 0; b < 2 && ok; b++)
+        ok = hipEventCreateWithFlags(&c->tev[b], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->rev[b], hipEventDisableTiming) == hipSuccess &&
+             halloc(c->h_off[b], nt + 1) && dalloc(c->rstage[b], fr) && dalloc(c->rpoff[b], nt) &&
+             dalloc(c->rcsz[b], nt) && dalloc(c->rres[b], nt) && halloc(c->h_stage[b], fr) &&
+             halloc(c->h_poff[b], nt) && halloc(c->h_csz[b], nt) && halloc(c->h_res[b], nt);
+    ok = ok && dalloc(c->txwin, (size_t)nconn * c->W) && dalloc(c->slots, nt * kChunkSlot) &&
+         dalloc(c->frames, fr) && dalloc(c->csz, nt) && dalloc(c->size, nt) && dalloc(c->pre, nt) &&
+         dalloc(c->cap, nt) && dalloc(c->src, nt) && dalloc(c->dst, nt) && dalloc(c->off, nt + 1) &&
+         hipMalloc(&c->scratch, APE_LZ4_frame_scratch_size(c->nt) + 16) == hipSuccess &&
+         halloc(c->h_frames, fr) && dalloc(c->rxwin, (size_t)nconn * c->W) && dalloc(c->rcap, nt) &&
+         dalloc(c->rdsz, nt) && dalloc(c->rsrc, nt) && dalloc(c->rdict, nt) && dalloc(c->rdst, nt);
+    if (!ok) {
+        chain_release(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void APE_LZ4_chain_free(APE_LZ4_chain *c) {
+    if (c) chain_release(c);
+}
+
+// TX: nmsg rounds; round m sends message m of every connection (at h_msgs + (m * nconn + i) *
+// msg_stride) as the reference's frames on fds[i].  Returns the bytes written or an error code.
+long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msgs,
+                             size_t msg_stride, int nmsg) {
+    if (!c || !fds || !h_msgs || nmsg < 0 || msg_stride < (size_t)c->msg) return APE_LZ4_GPU_EINVAL;
+    if (hipSetDevice(c->dev) != hipSuccess) return APE_LZ4_GPU_ENODEV;
+    const int nt = c->nt, nch = c->nch;
+    long long sent = 0;
+    int rc = 0;
+    auto launch = [&](int m) -> int {
+        const int b = m & 1;
+        const char *h = h_msgs + (size_t)m * c->nconn * msg_stride;
+        if (hipMemcpy2DAsync(c->txwin + c->txpos, c->W, h, msg_stride, (size_t)c->msg,
+                             (size_t)c->nconn, hipMemcpyHostToDevice, c->tst) != hipSuccess)
+            return APE_LZ4_GPU_ELAUNCH;
+        hipLaunchKernelGGL(chain_tx_setup, dim3((nt + 255) / 256), dim3(256), 0, c->tst, c->txwin,
+                           c->W, c->txpos, c->msg, nch, nt, c->slots, c->src, c->size, c->pre,
+                           c->dst, c->cap);
+        if (hipGetLastError() != hipSuccess) return APE_LZ4_GPU_ELAUNCH;
+        int r = APE_LZ4_compress_withPrefix_batch_dev(c->src, c->size, c->pre, c->dst, c->cap,
+                                                      c->csz, nt, c->tst);
+        if (r == 0) r = APE_LZ4_frame_offsets_dev(c->csz, c->off, c->scratch, nt, c->tst);
+        if (r == 0) r = APE_LZ4_frame_pack_strided_dev(c->slots, kChunkSlot, c->csz, c->off, c->frames, nt, c->tst);
+        if (r) return r;
+        if (hipMemcpyAsync(c->h_off[b], c->off, ((size_t)nt + 1) * sizeof(long long),
+                           hipMemcpyDeviceToHost, c->tst) != hipSuccess ||
+            hipEventRecord(c->tev[b], c->tst) != hipSuccess)
+            return APE_LZ4_GPU_ELAUNCH;
+        c->txpos += (uint32_t)c->msg;
+        return chain_slide(c->txwin, c->W, c->nconn, c->txpos, c->msg, c->tst) == hipSuccess
+                   ? 0 : APE_LZ4_GPU_ELAUNCH;
+    };
+    const long long t_all = now_ns();
+    if (nmsg > 0) rc = launch(0);
+    for (int m = 0; m < nmsg && rc == 0; m++) {
+        const int b = m & 1;
+        long long t0 = now_ns();
+        if (hipEventSynchronize(c->tev[b]) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        const long long *off = c->h_off[b];
+        const long long tot = off[nt];
+        // a chunk that did not fit its bound is a codec failure (never for valid sizes)
+        if (tot < 4ll * nt) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        if (hipMemcpyAsync(c->h_frames, c->frames, (size_t)tot, hipMemcpyDeviceToHost, c->tst) != hipSuccess ||
+            hipStreamSynchronize(c->tst) != hipSuccess) {
+            rc = APE_LZ4_GPU_ELAUNCH;
+            break;
+        }
+        sock_add(4, now_ns() - t0);
+        sock_add(5, 1);
+        if (m + 1 < nmsg) rc = launch(m + 1);   // the next round's GPU work under these writes
+        if (rc) break;
+        t0 = now_ns();
+        for (int i = 0; i < c->nconn && rc == 0; i++) {
+            const long long a = off[(size_t)i * nch], e = off[(size_t)(i + 1) * nch];
+            const long long w = write_all(fds[i], c->h_frames + a, (size_t)(e - a));
+            if (w < 0) rc = APE_LZ4_GPU_EINVAL;
+            else sent += w;
+        }
+        sock_add(3, now_ns() - t0);
+    }
+    if (hipStreamSynchronize(c->tst) != hipSuccess && rc == 0) rc = APE_LZ4_GPU_ELAUNCH;
+    sock_add(6, now_ns() - t_all);
+    return rc ? rc : sent;
+}
+
+// RX: nmsg rounds from every connection; round m decodes message m of connection i into
+// h_out + (m * nconn + i) * out_stride.  h_status[i] = 0, or the first failing chunk's result
+// (decompress_safe_continue's value, or the wrong size it produced); a failing connection
+// makes the call return APE_LZ4_GPU_EINVAL after the round.  Returns the payload bytes
+// delivered or an error code (EINVAL also for a malformed frame or an early EOF).
+long long APE_LZ4_chain_recv(APE_LZ4_chain *c, const int *fds, char *h_out, size_t out_stride,
+                             int nmsg, int *h_status) {
+    if (!c || !fds || !h_out || !h_status || nmsg < 0 || out_stride < (size_t)c->msg)
+        return APE_LZ4_GPU_EINVAL;
+    if (hipSetDevice(c->dev) != hipSuccess) return APE_LZ4_GPU_ENODEV;
+    const int M = c->nconn, nch = c->nch, nt = c->nt;
+    std::vector<APE_LZ4_rxbuf *> rb((size_t)M, nullptr);
+    std::vector<long long> offs((size_t)M * (nch + 1), 0);
+    std::vector<int> parsed((size_t)M, 0);
+    std::vector<char> eof((size_t)M, 0);
+    std::vector<pollfd> pf((size_t)M);
+    int rc = 0;
+    for (int i = 0; i < M; i++) {
+        h_status[i] = 0;
+        rb[i] = APE_LZ4_rxbuf_new(1u << 16);
+        if (!rb[i]) rc = APE_LZ4_GPU_ENOMEM;
+    }
+    long long got = 0;
+    bool busy[2] = {false, false};
+    int bround[2] = {0, 0};
+    auto check = [&](int b) {   // results of round bround[b] (its event has completed)
+        const int *r = c->h_res[b];
+        bool bad = false;
+        for (int k = 0; k < nch; k++) {
+            const int want = c->msg - kChunk * k < kChunk ? c->msg - kChunk * k : kChunk;
+            for (int i = 0; i < M; i++) {
+                const int v = r[(size_t)k * M + i];
+                if (v != want && h_status[i] == 0) {
+                    h_status[i] = v != 0 ? v : -1;
+                    bad = true;
+                }
+            }
+        }
+        if (!bad) got += (long long)M * c->msg;
+        busy[b] = false;
+        return bad ? APE_LZ4_GPU_EINVAL : 0;
+    };
+    const long long t_all = now_ns();
+    for (int m = 0; m < nmsg && rc == 0; m++) {
+        // ---- receive until every connection holds the round's nch frames (split-safe) ----
+        long long t0 = now_ns();
+        for (;;) {
+            int missing = 0, np = 0;
+            for (int i = 0; i < M; i++) {
+                if (parsed[i] < nch) {
+                    const int n = frames_from(rb[i], &offs[(size_t)i * (nch + 1)], parsed[i], nch, kChunkBound);
+                    if (n < 0) { rc = APE_LZ4_GPU_EINVAL; break; }
+                    parsed[i] = n;
+                }
+                if (parsed[i] < nch) {
+                    if (eof[i]) { rc = APE_LZ4_GPU_EINVAL; break; }
+                    pf[np].fd = fds[i];
+                    pf[np].events = POLLIN;
+                    pf[np].revents = 0;
+                    np++;
+                    missing++;
+                }
+            }
+            if (rc || missing == 0) break;
+            if (poll(pf.data(), (nfds_t)np, -1) < 0) {
+                if (errno == EINTR) continue;
+                rc = APE_LZ4_GPU_EINVAL;
+                break;
+            }
+            // read what arrived (the fd -> connection map is the order above)
+            for (int i = 0, q = 0; i < M && q < np && rc == 0; i++) {
+                if (parsed[i] >= nch) continue;
+                const short ev = pf[q++].revents;
+                if (!(ev & (POLLIN | POLLHUP | POLLERR))) continue;
+                APE_LZ4_rxbuf *b = rb[i];
+                if (APE_LZ4_rxbuf_prepare(b, 1u << 18) != 0) { rc = APE_LZ4_GPU_ENOMEM; break; }
+                const ssize_t r = read(fds[i], b->data + b->used, b->size - b->used);
+                if (r < 0) {
+                    if (errno == EINTR || errno == EAGAIN) continue;
+                    rc = APE_LZ4_GPU_EINVAL;
+                    break;
+                }
+                if (r == 0) eof[i] = 1;
+                b->used += (size_t)r;
+            }
+        }
+        sock_add(8, now_ns() - t0);
+        if (rc) break;
+        // ---- stage the round's payloads (packed, 16-byte aligned starts) ----
+        const int b = m & 1;
+        t0 = now_ns();
+        if (busy[b]) {   // round m - 2 used these buffers
+            if (hipEventSynchronize(c->rev[b]) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+            rc = check(b);
+            if (rc) break;
+        }
+        sock_add(13, now_ns() - t0);
+        t0 = now_ns();
+        size_t at = 0;
+        for (int i = 0; i < M; i++) {
+            const long long *o = &offs[(size_t)i * (nch + 1)];
+            for (int k = 0; k < nch; k++) {
+                const unsigned char *hp = (const unsigned char *)rb[i]->data + o[k];
+                const int sz = (int)((uint32_t)hp[0] | ((uint32_t)hp[1] << 8) | ((uint32_t)hp[2] << 16) |
+                                     ((uint32_t)hp[3] << 24));
+                memcpy(c->h_stage[b] + at, hp + 4, (size_t)sz);
+                c->h_poff[b][(size_t)i * nch + k] = (long long)at;
+                c->h_csz[b][(size_t)k * M + i] = sz;
+                at = (at + (size_t)sz + 15) & ~(size_t)15;
+            }
+            APE_LZ4_rxbuf_consume(rb[i], (size_t)o[nch]);
+            parsed[i] = 0;
+        }
+        sock_add(9, now_ns() - t0);
+        // ---- H2D, nch usingDict launches of M blocks, D2H into the caller's rows ----
+        hipError_t e = hipMemcpyAsync(c->rstage[b], c->h_stage[b], at + 16, hipMemcpyHostToDevice, c->rst);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->rpoff[b], c->h_poff[b], (size_t)nt * sizeof(long long), hipMemcpyHostToDevice, c->rst);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->rcsz[b], c->h_csz[b], (size_t)nt * sizeof(int), hipMemcpyHostToDevice, c->rst);
+        if (e != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        hipLaunchKernelGGL(chain_rx_setup, dim3((nt + 255) / 256), dim3(256), 0, c->rst, c->rstage[b],
+                           c->rpoff[b], c->rxwin, c->W, c->rxpos, c->msg, nch, M, c->rsrc, c->rdst,
+                           c->rcap, c->rdict, c->rdsz);
+        if (hipGetLastError() != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        for (int k = 0; k < nch && rc == 0; k++) {
+            const size_t e0 = (size_t)k * M;
+            rc = APE_LZ4_decompress_safe_usingDict_batch_dev(c->rsrc + e0, c->rcsz[b] + e0, c->rdst + e0,
+                                                             c->rcap + e0, c->rdict + e0, c->rdsz + e0,
+                                                             c->rres[b] + e0, M, c->rst);
+        }
+        if (rc) break;
+        e = hipMemcpy2DAsync(h_out + (size_t)m * M * out_stride, out_stride, c->rxwin + c->rxpos, c->W,
+                             (size_t)c->msg, (size_t)M, hipMemcpyDeviceToHost, c->rst);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->h_res[b], c->rres[b], (size_t)nt * sizeof(int), hipMemcpyDeviceToHost, c->rst);
+        if (e == hipSuccess) e = hipEventRecord(c->rev[b], c->rst);
+        if (e != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        busy[b] = true;
+        bround[b] = m;
+        sock_add(14, 1);
+        c->rxpos += (uint32_t)c->msg;
+        if (chain_slide(c->rxwin, c->W, M, c->rxpos, c->msg, c->rst) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+    }
+    // drain every round in flight, whatever rc is, before the buffers are reused
+    for (int b2 = 0; b2 < 2; b2++) {
+        const int b = (nmsg + b2) & 1;   // the older round first
+        if (!busy[b]) continue;
+        if (hipEventSynchronize(c->rev[b]) != hipSuccess) {
+            if (rc == 0) rc = APE_LZ4_GPU_ELAUNCH;
+            busy[b] = false;
+            continue;
+        }
+        const int r2 = check(b);
+        if (rc == 0) rc = r2;
+    }
+    sock_add(7, now_ns() - t_all);
+    for (int i = 0; i < M; i++) APE_LZ4_rxbuf_free(rb[i]);
+    return rc ? rc : got;
+}
+
+}  // extern "C"
+
+extern "C" {
 
 // Time split of the socket calls since the last reset (see g_sock_ns): out[16] in ms
 // (the two batch counts as counts).  reset != 0 zeroes the accumulators afterwards.

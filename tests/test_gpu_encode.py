@@ -187,6 +187,9 @@ def test_block_limit(cuda, product):
     assert rs == [product.ERANGE]
 
 
+ACCEL_RATIO_TOL = 0.05   # |GPU / reference - 1| at acceleration 2, 4, 8 (measured: DESIGN 3.1)
+
+
 def test_acceleration(cuda, product, oracle):
     """compress_fast with acceleration > 1 (ref src/ape_lz4.c:789-808, step = searchMatchNb
     >> 6 from acceleration << 6, :597-600): valid blocks at a ratio that falls as the
@@ -211,9 +214,16 @@ def test_acceleration(cuda, product, oracle):
     rs1, comps1 = run_encode(cuda, product, srcs)
     assert out[1][1] == comps1
     ratio = {a: 32 * 65536 / sum(out[a][0][:32]) for a in out}
-    print("ratio by acceleration", {a: round(r, 4) for a, r in ratio.items()})
+    # the reference's compress_fast on the same blocks (its probe pattern, step growth after
+    # 64 misses included, is what the GPU walker follows: VERDICT r3 item 8)
+    ref = {a: 32 * 65536 / sum(orc_compress(oracle, s, accel=a)[0] for s in srcs[:32])
+           for a in (1, 2, 4, 8)}
+    print("ratio by acceleration", {a: round(r, 4) for a, r in ratio.items()},
+          "reference", {a: round(r, 4) for a, r in ref.items()})
     assert ratio[1] >= ratio[2] > ratio[4] > ratio[8] > ratio[1 << 30]
     assert ratio[2] >= 0.9 * ratio[1]
+    for a in (2, 4, 8):
+        assert abs(ratio[a] / ref[a] - 1.0) <= ACCEL_RATIO_TOL, (a, ratio[a], ref[a])
     # a huge acceleration probes only the three positions after each match end (and the
     # block's first three): little is found, but the blocks stay valid (checked above)
     assert ratio[1 << 30] < 1.5

@@ -14,6 +14,7 @@ import threading
 
 import numpy as np
 import pytest
+from lz4util import I
 
 
 def frame(blocks):
@@ -241,3 +242,263 @@ def test_cpu_sock_baseline_times_codec_only(oracle):
         assert lib.cpu_sock_run(path.encode(), prefix, nconn, msg, nmsg, kind, out) == 0
         assert out[3] == 0 and out[1] == nconn * msg * nmsg and out[0] > 0
         assert out[2] > 4 * nconn * nmsg * ((msg + 8191) // 8192)
+
+
+# ---------------- chained streams: the reference wire format through the GPU ----------------
+def _ref_peer():
+    """The reference codec itself (oracle/_ref, compiled from src/ape_lz4.c) as the peer of
+    the GPU chain; the restatement where _ref is absent."""
+    import ctypes as C
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ref = os.path.join(root, "oracle", "_ref", "libape_lz4_ref.so")
+    if os.path.exists(ref):
+        L, pre = C.CDLL(ref), "APE_LZ4_"
+    else:
+        L, pre = C.CDLL(os.path.join(root, "oracle", "liblz4_oracle.so")), "orc_"
+    f = {}
+    for name, res, args in (("createStream", C.c_void_p, []), ("freeStream", C.c_int, [C.c_void_p]),
+                            ("createStreamDecode", C.c_void_p, []),
+                            ("freeStreamDecode", C.c_int, [C.c_void_p]),
+                            ("compress_fast_continue", C.c_int,
+                             [C.c_void_p, C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int]),
+                            ("saveDict", C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+                            ("decompress_safe_continue", C.c_int,
+                             [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
+                            ("setStreamDecode", C.c_int, [C.c_void_p, C.c_void_p, C.c_int])):
+        fn = getattr(L, pre + name)
+        fn.restype, fn.argtypes = res, args
+        f[name] = fn
+    return f
+
+
+def _ref_tx(peer, msgs):
+    """ape_socket_write's LZ4 path (src/ape_socket.c:811-871) for one connection: every
+    message in 8 KiB chunks, compress_fast_continue into [int32 size][block], saveDict."""
+    import ctypes as C
+    st = C.c_void_p(peer["createStream"]())
+    dictbuf = C.create_string_buffer(65536)
+    out, keep = bytearray(), []
+    for msg in msgs:
+        mb = C.create_string_buffer(bytes(msg), len(msg) + 16)
+        keep.append(mb)
+        for pos in range(0, len(msg), 8192):
+            ln = min(8192, len(msg) - pos)
+            ob = C.create_string_buffer(8240 + 64)
+            r = peer["compress_fast_continue"](st, C.cast(C.byref(mb, pos), C.c_char_p), ob, ln, 8240, 1)
+            assert r > 0
+            out += r.to_bytes(4, "little") + ob.raw[:r]
+        peer["saveDict"](st, dictbuf, 65536)
+    peer["freeStream"](st)
+    return bytes(out)
+
+
+def _ref_rx(peer, stream):
+    """ape_socket_read_lz4_stream's decode (:1386-1421) for one connection: each frame with
+    decompress_safe_continue into an 8 KiB buffer, appended to the 64 KiB dictionary buffer
+    (memmove when full), setStreamDecode on it.  Returns the plain bytes (None on an error)."""
+    import ctypes as C
+    sd = C.c_void_p(peer["createStreamDecode"]())
+    ring = C.create_string_buffer(65536)
+    rp, p, plain = 0, 0, bytearray()
+    while p < len(stream):
+        sz = int.from_bytes(stream[p:p + 4], "little", signed=True)
+        if sz <= 0 or sz > 8240 or p + 4 + sz > len(stream):
+            return None
+        blk = C.create_string_buffer(stream[p + 4:p + 4 + sz], sz + 16)
+        tmp = C.create_string_buffer(8192 + 64)
+        r = peer["decompress_safe_continue"](sd, blk, tmp, sz, 8192)
+        if r <= 0:
+            return None
+        if rp + r > 65536:
+            need = r - (65536 - rp)
+            C.memmove(ring, C.byref(ring, need), rp - need)
+            C.memmove(C.byref(ring, rp - need), tmp, r)
+            rp = 65536
+        else:
+            C.memmove(C.byref(ring, rp), tmp, r)
+            rp += r
+        peer["setStreamDecode"](sd, ring, rp)
+        plain += tmp.raw[:r]
+        p += 4 + sz
+    peer["freeStreamDecode"](sd)
+    return bytes(plain)
+
+
+def _chain_msgs(cuda, product, nmsg, nconn, msg_len, seed):
+    rng = random.Random(seed)
+    msgs = np.zeros((nmsg, nconn, msg_len), dtype=np.uint8)
+    for m in range(nmsg):
+        for i in range(nconn):
+            kind = rng.choice(["comp", "comp", "text", "rand"])
+            msgs[m, i] = np.frombuffer(I.make(kind, msg_len, seed=seed * 1000 + m * nconn + i), dtype=np.uint8)
+    return msgs
+
+
+def _drain(sock):
+    out = bytearray()
+    while True:
+        b = sock.recv(1 << 20)
+        if not b:
+            return bytes(out)
+        out += b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("msg_len,nmsg", [(65536, 6), (25576, 5)])
+def test_chain_gpu_tx_decoded_by_reference(cuda, product, msg_len, nmsg):
+    """GPU chain_send writes the reference's wire format: the reference's own
+    decompress_safe_continue + 64 KiB dictionary ring (ape_socket.c:1386-1421) restores every
+    message of every connection, across window slides (6 x 64 KiB > 2 x 64 KiB + 64 KiB)."""
+    nconn = 5
+    peer = _ref_peer()
+    msgs = _chain_msgs(cuda, product, nmsg, nconn, msg_len, seed=msg_len)
+    pairs = [_pair() for _ in range(nconn)]
+    ch = product.Chain(nconn, msg_len)
+    res = {}
+
+    def txf():
+        try:
+            res["sent"] = ch.send([t.fileno() for t, _ in pairs], msgs)
+        finally:
+            for t, _ in pairs:
+                t.shutdown(socket.SHUT_WR)
+
+    th = threading.Thread(target=txf)
+    th.start()
+    streams = [None] * nconn
+    readers = [threading.Thread(target=lambda i=i: streams.__setitem__(i, _drain(pairs[i][1])))
+               for i in range(nconn)]
+    for r in readers:
+        r.start()
+    for r in readers:
+        r.join()
+    th.join()
+    ch.free()
+    for t, r in pairs:
+        t.close()
+        r.close()
+    assert res["sent"] == sum(len(s) for s in streams)
+    nch = (msg_len + 8191) // 8192
+    for i in range(nconn):
+        plain = _ref_rx(peer, streams[i])
+        assert plain == msgs[:, i, :].tobytes(), i
+        # frame count: nch per message, sizes within the chunk bound
+        p, nf = 0, 0
+        while p < len(streams[i]):
+            sz = int.from_bytes(streams[i][p:p + 4], "little")
+            assert 0 < sz <= 8240
+            p += 4 + sz
+            nf += 1
+        assert nf == nch * nmsg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("msg_len,nmsg,pieces", [(65536, 6, False), (25576, 4, True)])
+def test_chain_reference_tx_decoded_by_gpu(cuda, product, msg_len, nmsg, pieces):
+    """GPU chain_recv reads the reference's wire format: frames from the reference's own
+    compress_fast_continue + saveDict (ape_socket.c:811-871) decode bit-exactly, also when the
+    sender writes them in 1-7-byte and random pieces (every header split: the K7 parser)."""
+    nconn = 4
+    peer = _ref_peer()
+    msgs = _chain_msgs(cuda, product, nmsg, nconn, msg_len, seed=msg_len + 1)
+    streams = [_ref_tx(peer, [msgs[m, i].tobytes() for m in range(nmsg)]) for i in range(nconn)]
+    pairs = [_pair() for _ in range(nconn)]
+
+    def txf(i):
+        t = pairs[i][0]
+        if pieces:
+            _send_pieces(t, streams[i], random.Random(i), 30000)
+        else:
+            t.sendall(streams[i])
+            t.shutdown(socket.SHUT_WR)
+
+    ths = [threading.Thread(target=txf, args=(i,)) for i in range(nconn)]
+    for t in ths:
+        t.start()
+    out = np.full((nmsg, nconn, msg_len + 32), 0xCB, dtype=np.uint8)
+    status = np.full(nconn, -9, dtype=np.int32)
+    ch = product.Chain(nconn, msg_len)
+    got = ch.recv([r.fileno() for _, r in pairs], out, status)
+    ch.free()
+    for t in ths:
+        t.join()
+    for t, r in pairs:
+        t.close()
+        r.close()
+    assert got == nmsg * nconn * msg_len and (status == 0).all()
+    assert np.array_equal(out[:, :, :msg_len], msgs)
+    assert (out[:, :, msg_len:] == 0xCB).all()
+
+
+@pytest.mark.gpu
+def test_chain_gpu_roundtrip_and_malformed(cuda, product):
+    """GPU TX -> loopback -> GPU RX over 8 connections, every byte compared; then a stream
+    with one mutated block fails that connection (status != 0, GpuError), and a truncated one
+    raises (early EOF)."""
+    nconn, msg_len, nmsg = 8, 65536, 5
+    msgs = _chain_msgs(cuda, product, nmsg, nconn, msg_len, seed=7)
+    pairs = [_pair() for _ in range(nconn)]
+    tx, rx = product.Chain(nconn, msg_len), product.Chain(nconn, msg_len)
+
+    def txf():
+        try:
+            tx.send([t.fileno() for t, _ in pairs], msgs)
+        finally:
+            for t, _ in pairs:
+                t.shutdown(socket.SHUT_WR)
+
+    th = threading.Thread(target=txf)
+    th.start()
+    out = np.zeros((nmsg, nconn, msg_len), dtype=np.uint8)
+    status = np.full(nconn, -9, dtype=np.int32)
+    got = rx.recv([r.fileno() for _, r in pairs], out, status)
+    th.join()
+    for t, r in pairs:
+        t.close()
+        r.close()
+    assert got == nmsg * nconn * msg_len and (status == 0).all() and np.array_equal(out, msgs)
+    tx.free()
+    rx.free()
+    # damaged streams from the reference sender
+    peer = _ref_peer()
+    for damage in ("mutated", "truncated"):
+        streams = [bytearray(_ref_tx(peer, [msgs[m, i].tobytes() for m in range(2)]))
+                   for i in range(3)]
+        if damage == "mutated":   # connection 1: the third frame's first literal run -> bad offset
+            p = 0
+            for _ in range(2):
+                p += 4 + int.from_bytes(streams[1][p:p + 4], "little")
+            streams[1][p + 4] = 0x0F   # token: no literals, match, then offset bytes of the payload
+            streams[1][p + 5] = 0xFF
+            streams[1][p + 6] = 0xFF
+        else:
+            streams[2] = streams[2][:-50]
+        pairs = [_pair() for _ in range(3)]
+        for (t, _), s in zip(pairs, streams):
+            threading.Thread(target=lambda t=t, s=s: (t.sendall(bytes(s)), t.shutdown(socket.SHUT_WR))).start()
+        ch = product.Chain(3, msg_len)
+        out = np.zeros((2, 3, msg_len), dtype=np.uint8)
+        status = np.zeros(3, dtype=np.int32)
+        with pytest.raises(product.GpuError):
+            ch.recv([r.fileno() for _, r in pairs], out, status)
+        ch.free()
+        for t, r in pairs:
+            t.close()
+            r.close()
+        if damage == "mutated":
+            assert status[1] != 0 and status[0] == 0 and status[2] == 0
+
+
+def test_chain_reference_peer_matches_golden(golden):
+    """The test-side reference peer (_ref_tx / _ref_rx: ape_socket.c's codec calls on the
+    reference library) reproduces the golden socket-stream KATs byte for byte, so the GPU
+    chain tests above compare against the reference's own wire format."""
+    import base64
+    peer = _ref_peer()
+    for kat in golden["stream"]:
+        msgs = [I.make(kat["content"], kat["msg_len"], seed=s) for s in kat["seeds"]]
+        want = b"".join(len(base64.b64decode(f)).to_bytes(4, "little") + base64.b64decode(f)
+                        for f in kat["frames_b64"])
+        assert _ref_tx(peer, msgs) == want, kat["content"]
+        assert _ref_rx(peer, want) == b"".join(msgs)
