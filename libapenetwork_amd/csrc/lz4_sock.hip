@@ -470,16 +470,16 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
 // <= 64 KiB of the connection's stream and framed [int32 size][block] (:811-871; saveDict
 // after the message keeps the history, :856); the receiver decodes each frame with
 // decompress_safe_continue against its 64 KiB dictionary buffer (:1386-1421).  A server holds
-// many connections, so the GPU batches them:
-//   TX: one message per connection per round.  A chunk's history is plaintext the sender
-//       already has, so all chunks of the round (nconn x nch) are compressed in ONE
-//       withPrefix launch, each against the bytes before it in its connection's device
-//       window; frames are packed on the GPU and written to each connection's socket.
-//   RX: per connection a receive buffer with the split-safe parser; a round takes one
-//       message (nch frames) from every connection and decodes it with nch usingDict
-//       launches of nconn blocks each (chunk k + 1's dictionary is chunk k's output, so
-//       the chunks of one stream are sequential; the connections are the batch).
-// Both sides keep a window of W bytes per connection on the device; when the next message
+// many connections, so the GPU batches them, K messages per connection per round:
+//   TX: a chunk's history is plaintext the sender already has, so every chunk of the round
+//       (nconn x K x nch) is compressed in ONE withPrefix launch, each against the bytes
+//       before it in its connection's device window; the frames are packed on the GPU and
+//       each connection's frames of the round are written to its socket with one write().
+//   RX: per connection a receive buffer with the split-safe parser; a round takes K messages
+//       (K x nch frames) from every connection and decodes them with K x nch usingDict
+//       launches of nconn blocks each (chunk q + 1's dictionary is chunk q's output: the
+//       chunks of one stream are sequential, the connections are the batch).
+// Both sides keep a window of W bytes per connection on the device; when the next round
 // would pass its end, the last 64 KiB move to its start (one 2-D device copy for all).
 // Bytes on the wire: exactly the reference's format, so an unmodified reference peer reads
 // what chain_send writes and writes what chain_recv reads (tests/test_sock.py).
@@ -489,35 +489,39 @@ constexpr int kChunk = 8192;                      // APE_LZ4_BLOCK_SIZE (:39)
 constexpr int kChunkBound = kChunk + kChunk / 255 + 16;   // APE_LZ4_COMPRESSBOUND(8192)
 constexpr size_t kChunkSlot = (kChunkBound + 15) & ~15;
 constexpr int kHist = 65536;                      // the dictionary (:43)
+constexpr size_t kRoundBytes = 32u << 20;         // payload per round (all connections)
 
-// TX pointer arrays of a round: chunk t = (connection i, chunk j), t = i * nch + j
-__global__ void chain_tx_setup(char *win, size_t W, uint32_t pos, int msg, int nch, int n,
+// TX pointer arrays of a round of k messages: chunk t = (connection i, message mm, chunk j),
+// t = (i * k + mm) * nch + j -- connection-major, so a connection's frames are contiguous
+__global__ void chain_tx_setup(char *win, size_t W, uint32_t pos, int msg, int nch, int k, int n,
                                char *slots, const char **src, int *size, int *pre, char **dst,
                                int *cap) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    const int i = t / nch, j = t - i * nch;
+    const int i = t / (k * nch), r = t - i * k * nch, mm = r / nch, j = r - mm * nch;
     const int len = msg - kChunk * j < kChunk ? msg - kChunk * j : kChunk;
-    src[t] = win + (size_t)i * W + pos + (size_t)kChunk * j;
+    const uint32_t at = pos + (uint32_t)mm * (uint32_t)msg + (uint32_t)(kChunk * j);
+    src[t] = win + (size_t)i * W + at;
     size[t] = len;
-    pre[t] = (int)pos + kChunk * j;   // the whole stream so far (the encoder keeps what fits)
+    pre[t] = (int)at;   // the whole stream so far (the encoder keeps what fits its window)
     dst[t] = slots + (size_t)t * kChunkSlot;
     cap[t] = len + len / 255 + 16;
 }
 
-// RX pointer arrays of a round, chunk-major (launch k decodes entries [k * nconn, (k+1) * nconn)):
-// entry k * nconn + i = chunk k of connection i, payload at stage + poff[i * nch + k]
+// RX pointer arrays of a round, chunk-major: launch q (= mm * nch + j) decodes entries
+// [q * nconn, (q + 1) * nconn); entry q * nconn + i = chunk q of connection i, its payload at
+// stage + poff[i * k * nch + q]
 __global__ void chain_rx_setup(const char *stage, const long long *poff, char *win, size_t W,
-                               uint32_t pos, int msg, int nch, int nconn, const char **src,
+                               uint32_t pos, int msg, int nch, int k, int nconn, const char **src,
                                char **dst, int *cap, const char **dict, int *dsz) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= nch * nconn) return;
-    const int k = e / nconn, i = e - k * nconn;
-    const uint32_t at = pos + (uint32_t)(kChunk * k);
+    if (e >= k * nch * nconn) return;
+    const int q = e / nconn, i = e - q * nconn, mm = q / nch, j = q - mm * nch;
+    const uint32_t at = pos + (uint32_t)mm * (uint32_t)msg + (uint32_t)(kChunk * j);
     const uint32_t h = at < (uint32_t)kHist ? at : (uint32_t)kHist;
-    src[e] = stage + poff[i * nch + k];
+    src[e] = stage + poff[(size_t)i * k * nch + q];
     dst[e] = win + (size_t)i * W + at;
-    cap[e] = msg - kChunk * k < kChunk ? msg - kChunk * k : kChunk;
+    cap[e] = msg - kChunk * j < kChunk ? msg - kChunk * j : kChunk;
     dict[e] = win + (size_t)i * W + at - h;
     dsz[e] = (int)h;
 }
@@ -525,7 +529,7 @@ __global__ void chain_rx_setup(const char *stage, const long long *poff, char *w
 }  // namespace
 
 struct APE_LZ4_chain {
-    int dev = 0, nconn = 0, msg = 0, nch = 0, nt = 0;
+    int dev = 0, nconn = 0, msg = 0, nch = 0, K = 1, nt = 0;   // nt = chunks of a full round
     size_t W = 0;
     // TX (one thread): device window, compressed slots, frames, pointer arrays
     hipStream_t tst = nullptr;
@@ -585,17 +589,19 @@ bool halloc(T *&p, size_t n) {
     return hipHostMalloc((void **)&p, n * sizeof(T), hipHostMallocDefault) == hipSuccess;
 }
 
-// the window slides when the next message would pass its end: the last <= 64 KiB of every
-// connection's stream move to the start of its row (a 2-D device copy; rows never overlap
-// their source since W >= 2 x 64 KiB + msg)
-hipError_t chain_slide(char *win, size_t W, int nconn, uint32_t &pos, int msg, hipStream_t st) {
-    if ((size_t)pos + (size_t)msg <= W) return hipSuccess;
+// the window slides when the next round (`need` bytes) would pass its end: the last <= 64 KiB
+// of every connection's stream move to the start of its row (a 2-D device copy; a row never
+// overlaps its source since W >= 2 x 64 KiB + a round)
+hipError_t chain_slide(char *win, size_t W, int nconn, uint32_t &pos, size_t need, hipStream_t st) {
+    if ((size_t)pos + need <= W) return hipSuccess;
     const uint32_t keep = pos < (uint32_t)kHist ? pos : (uint32_t)kHist;
     const hipError_t e = hipMemcpy2DAsync(win, W, win + (pos - keep), W, keep, (size_t)nconn,
                                           hipMemcpyDeviceToDevice, st);
     pos = keep;
     return e;
 }
+
+inline int chunk_len(int msg, int j) { return msg - kChunk * j < kChunk ? msg - kChunk * j : kChunk; }
 
 }  // namespace
 
@@ -608,8 +614,14 @@ APE_LZ4_chain *APE_LZ4_chain_new(int nconn, int msg_len) {
     c->nconn = nconn;
     c->msg = msg_len;
     c->nch = (msg_len + kChunk - 1) / kChunk;
-    c->nt = nconn * c->nch;
-    c->W = ((size_t)2 * kHist + (size_t)msg_len + 255) & ~(size_t)255;
+    const size_t per = (size_t)nconn * (size_t)msg_len;
+    c->K = (int)(per >= kRoundBytes ? 1 : (kRoundBytes / per < 16 ? kRoundBytes / per : 16));
+    if (const char *ev = getenv("APE_LZ4_CHAIN_ROUND")) {   // messages per round (tests: many rounds)
+        const int k = atoi(ev);
+        if (k >= 1 && k <= 64) c->K = k;
+    }
+    c->nt = nconn * c->K * c->nch;
+    c->W = ((size_t)2 * kHist + (size_t)c->K * msg_len + 255) & ~(size_t)255;
     const size_t nt = (size_t)c->nt, fr = nt * (kChunkSlot + 4) + 64;
     bool ok = hipStreamCreateWithFlags(&c->tst, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->rst, hipStreamNonBlocking) == hipSuccess;
@@ -636,48 +648,53 @@ void APE_LZ4_chain_free(APE_LZ4_chain *c) {
     if (c) chain_release(c);
 }
 
-// TX: nmsg rounds; round m sends message m of every connection (at h_msgs + (m * nconn + i) *
-// msg_stride) as the reference's frames on fds[i].  Returns the bytes written or an error code.
+// TX: nmsg messages per connection (message m of connection i at h_msgs + (m * nconn + i) *
+// msg_stride) as the reference's frames on fds[i], in rounds of K messages.  Returns the bytes
+// written or an error code.
 long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msgs,
                              size_t msg_stride, int nmsg) {
     if (!c || !fds || !h_msgs || nmsg < 0 || msg_stride < (size_t)c->msg) return APE_LZ4_GPU_EINVAL;
     if (hipSetDevice(c->dev) != hipSuccess) return APE_LZ4_GPU_ENODEV;
-    const int nt = c->nt, nch = c->nch;
+    const int M = c->nconn, nch = c->nch, nr = (nmsg + c->K - 1) / c->K;
     long long sent = 0;
     int rc = 0;
-    auto launch = [&](int m) -> int {
-        const int b = m & 1;
-        const char *h = h_msgs + (size_t)m * c->nconn * msg_stride;
-        if (hipMemcpy2DAsync(c->txwin + c->txpos, c->W, h, msg_stride, (size_t)c->msg,
-                             (size_t)c->nconn, hipMemcpyHostToDevice, c->tst) != hipSuccess)
+    auto round_k = [&](int r) { return nmsg - r * c->K < c->K ? nmsg - r * c->K : c->K; };
+    auto launch = [&](int r) -> int {
+        const int b = r & 1, k = round_k(r), nt = M * k * nch;
+        if (chain_slide(c->txwin, c->W, M, c->txpos, (size_t)k * c->msg, c->tst) != hipSuccess)
             return APE_LZ4_GPU_ELAUNCH;
+        for (int mm = 0; mm < k; mm++) {
+            const char *h = h_msgs + (size_t)(r * c->K + mm) * M * msg_stride;
+            if (hipMemcpy2DAsync(c->txwin + c->txpos + (size_t)mm * c->msg, c->W, h, msg_stride,
+                                 (size_t)c->msg, (size_t)M, hipMemcpyHostToDevice, c->tst) != hipSuccess)
+                return APE_LZ4_GPU_ELAUNCH;
+        }
         hipLaunchKernelGGL(chain_tx_setup, dim3((nt + 255) / 256), dim3(256), 0, c->tst, c->txwin,
-                           c->W, c->txpos, c->msg, nch, nt, c->slots, c->src, c->size, c->pre,
+                           c->W, c->txpos, c->msg, nch, k, nt, c->slots, c->src, c->size, c->pre,
                            c->dst, c->cap);
         if (hipGetLastError() != hipSuccess) return APE_LZ4_GPU_ELAUNCH;
-        int r = APE_LZ4_compress_withPrefix_batch_dev(c->src, c->size, c->pre, c->dst, c->cap,
+        int e = APE_LZ4_compress_withPrefix_batch_dev(c->src, c->size, c->pre, c->dst, c->cap,
                                                       c->csz, nt, c->tst);
-        if (r == 0) r = APE_LZ4_frame_offsets_dev(c->csz, c->off, c->scratch, nt, c->tst);
-        if (r == 0) r = APE_LZ4_frame_pack_strided_dev(c->slots, kChunkSlot, c->csz, c->off, c->frames, nt, c->tst);
-        if (r) return r;
+        if (e == 0) e = APE_LZ4_frame_offsets_dev(c->csz, c->off, c->scratch, nt, c->tst);
+        if (e == 0) e = APE_LZ4_frame_pack_strided_dev(c->slots, kChunkSlot, c->csz, c->off, c->frames, nt, c->tst);
+        if (e) return e;
         if (hipMemcpyAsync(c->h_off[b], c->off, ((size_t)nt + 1) * sizeof(long long),
                            hipMemcpyDeviceToHost, c->tst) != hipSuccess ||
             hipEventRecord(c->tev[b], c->tst) != hipSuccess)
             return APE_LZ4_GPU_ELAUNCH;
-        c->txpos += (uint32_t)c->msg;
-        return chain_slide(c->txwin, c->W, c->nconn, c->txpos, c->msg, c->tst) == hipSuccess
-                   ? 0 : APE_LZ4_GPU_ELAUNCH;
+        c->txpos += (uint32_t)(k * c->msg);
+        return 0;
     };
     const long long t_all = now_ns();
-    if (nmsg > 0) rc = launch(0);
-    for (int m = 0; m < nmsg && rc == 0; m++) {
-        const int b = m & 1;
+    if (nr > 0) rc = launch(0);
+    for (int r = 0; r < nr && rc == 0; r++) {
+        const int b = r & 1, k = round_k(r), nt = M * k * nch;
         long long t0 = now_ns();
         if (hipEventSynchronize(c->tev[b]) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
         const long long *off = c->h_off[b];
         const long long tot = off[nt];
         // a chunk that did not fit its bound is a codec failure (never for valid sizes)
-        if (tot < 4ll * nt) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        if (tot <= 4ll * nt) { rc = APE_LZ4_GPU_ELAUNCH; break; }
         if (hipMemcpyAsync(c->h_frames, c->frames, (size_t)tot, hipMemcpyDeviceToHost, c->tst) != hipSuccess ||
             hipStreamSynchronize(c->tst) != hipSuccess) {
             rc = APE_LZ4_GPU_ELAUNCH;
@@ -685,11 +702,11 @@ long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msg
         }
         sock_add(4, now_ns() - t0);
         sock_add(5, 1);
-        if (m + 1 < nmsg) rc = launch(m + 1);   // the next round's GPU work under these writes
+        if (r + 1 < nr) rc = launch(r + 1);   // the next round's GPU work under these writes
         if (rc) break;
         t0 = now_ns();
-        for (int i = 0; i < c->nconn && rc == 0; i++) {
-            const long long a = off[(size_t)i * nch], e = off[(size_t)(i + 1) * nch];
+        for (int i = 0; i < M && rc == 0; i++) {   // connection i's frames of the round
+            const long long a = off[(size_t)i * k * nch], e = off[(size_t)(i + 1) * k * nch];
             const long long w = write_all(fds[i], c->h_frames + a, (size_t)(e - a));
             if (w < 0) rc = APE_LZ4_GPU_EINVAL;
             else sent += w;
@@ -701,153 +718,160 @@ long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msg
     return rc ? rc : sent;
 }
 
-// RX: nmsg rounds from every connection; round m decodes message m of connection i into
+// RX: nmsg messages per connection, in rounds of K; message m of connection i is decoded into
 // h_out + (m * nconn + i) * out_stride.  h_status[i] = 0, or the first failing chunk's result
 // (decompress_safe_continue's value, or the wrong size it produced); a failing connection
-// makes the call return APE_LZ4_GPU_EINVAL after the round.  Returns the payload bytes
-// delivered or an error code (EINVAL also for a malformed frame or an early EOF).
+// makes the call return APE_LZ4_GPU_EINVAL.  Returns the payload bytes delivered or an error
+// code (EINVAL also for a malformed frame or an early EOF).
 long long APE_LZ4_chain_recv(APE_LZ4_chain *c, const int *fds, char *h_out, size_t out_stride,
                              int nmsg, int *h_status) {
     if (!c || !fds || !h_out || !h_status || nmsg < 0 || out_stride < (size_t)c->msg)
         return APE_LZ4_GPU_EINVAL;
     if (hipSetDevice(c->dev) != hipSuccess) return APE_LZ4_GPU_ENODEV;
-    const int M = c->nconn, nch = c->nch, nt = c->nt;
+    const int M = c->nconn, nch = c->nch, nr = (nmsg + c->K - 1) / c->K;
+    const int maxf = c->K * nch;   // frames of a full round per connection
     std::vector<APE_LZ4_rxbuf *> rb((size_t)M, nullptr);
-    std::vector<long long> offs((size_t)M * (nch + 1), 0);
+    std::vector<long long> offs((size_t)M * (maxf + 1), 0);
     std::vector<int> parsed((size_t)M, 0);
     std::vector<char> eof((size_t)M, 0);
     std::vector<pollfd> pf((size_t)M);
+    std::vector<int> pmap((size_t)M);
     int rc = 0;
     for (int i = 0; i < M; i++) {
         h_status[i] = 0;
         rb[i] = APE_LZ4_rxbuf_new(1u << 16);
         if (!rb[i]) rc = APE_LZ4_GPU_ENOMEM;
     }
+    auto round_k = [&](int r) { return nmsg - r * c->K < c->K ? nmsg - r * c->K : c->K; };
     long long got = 0;
     bool busy[2] = {false, false};
-    int bround[2] = {0, 0};
-    auto check = [&](int b) {   // results of round bround[b] (its event has completed)
-        const int *r = c->h_res[b];
+    int bk[2] = {0, 0};   // messages of the round in flight on slot b
+    auto check = [&](int b) {   // results of the round on slot b (its event has completed)
+        const int *res = c->h_res[b];
         bool bad = false;
-        for (int k = 0; k < nch; k++) {
-            const int want = c->msg - kChunk * k < kChunk ? c->msg - kChunk * k : kChunk;
+        for (int q = 0; q < bk[b] * nch; q++) {
+            const int want = chunk_len(c->msg, q % nch);
             for (int i = 0; i < M; i++) {
-                const int v = r[(size_t)k * M + i];
+                const int v = res[(size_t)q * M + i];
                 if (v != want && h_status[i] == 0) {
                     h_status[i] = v != 0 ? v : -1;
                     bad = true;
                 }
             }
         }
-        if (!bad) got += (long long)M * c->msg;
+        if (!bad) got += (long long)M * bk[b] * c->msg;
         busy[b] = false;
         return bad ? APE_LZ4_GPU_EINVAL : 0;
     };
     const long long t_all = now_ns();
-    for (int m = 0; m < nmsg && rc == 0; m++) {
-        // ---- receive until every connection holds the round's nch frames (split-safe) ----
+    for (int r = 0; r < nr && rc == 0; r++) {
+        const int k = round_k(r), nf = k * nch, ne = M * nf;
+        // ---- receive until every connection holds the round's k x nch frames (split-safe) ----
         long long t0 = now_ns();
         for (;;) {
-            int missing = 0, np = 0;
+            int np = 0;
             for (int i = 0; i < M; i++) {
-                if (parsed[i] < nch) {
-                    const int n = frames_from(rb[i], &offs[(size_t)i * (nch + 1)], parsed[i], nch, kChunkBound);
+                long long *o = &offs[(size_t)i * (maxf + 1)];
+                if (parsed[i] < nf) {
+                    const int n = frames_from(rb[i], o, parsed[i], nf, kChunkBound);
                     if (n < 0) { rc = APE_LZ4_GPU_EINVAL; break; }
                     parsed[i] = n;
                 }
-                if (parsed[i] < nch) {
+                if (parsed[i] < nf) {
                     if (eof[i]) { rc = APE_LZ4_GPU_EINVAL; break; }
                     pf[np].fd = fds[i];
                     pf[np].events = POLLIN;
                     pf[np].revents = 0;
-                    np++;
-                    missing++;
+                    pmap[np++] = i;
                 }
             }
-            if (rc || missing == 0) break;
+            if (rc || np == 0) break;
             if (poll(pf.data(), (nfds_t)np, -1) < 0) {
                 if (errno == EINTR) continue;
                 rc = APE_LZ4_GPU_EINVAL;
                 break;
             }
-            // read what arrived (the fd -> connection map is the order above)
-            for (int i = 0, q = 0; i < M && q < np && rc == 0; i++) {
-                if (parsed[i] >= nch) continue;
-                const short ev = pf[q++].revents;
-                if (!(ev & (POLLIN | POLLHUP | POLLERR))) continue;
-                APE_LZ4_rxbuf *b = rb[i];
-                if (APE_LZ4_rxbuf_prepare(b, 1u << 18) != 0) { rc = APE_LZ4_GPU_ENOMEM; break; }
-                const ssize_t r = read(fds[i], b->data + b->used, b->size - b->used);
-                if (r < 0) {
+            for (int q = 0; q < np && rc == 0; q++) {
+                if (!(pf[q].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+                const int i = pmap[q];
+                APE_LZ4_rxbuf *bf = rb[i];
+                if (APE_LZ4_rxbuf_prepare(bf, 1u << 18) != 0) { rc = APE_LZ4_GPU_ENOMEM; break; }
+                const ssize_t n = read(fds[i], bf->data + bf->used, bf->size - bf->used);
+                if (n < 0) {
                     if (errno == EINTR || errno == EAGAIN) continue;
                     rc = APE_LZ4_GPU_EINVAL;
                     break;
                 }
-                if (r == 0) eof[i] = 1;
-                b->used += (size_t)r;
+                if (n == 0) eof[i] = 1;
+                bf->used += (size_t)n;
             }
         }
         sock_add(8, now_ns() - t0);
         if (rc) break;
-        // ---- stage the round's payloads (packed, 16-byte aligned starts) ----
-        const int b = m & 1;
+        const int b = r & 1;
         t0 = now_ns();
-        if (busy[b]) {   // round m - 2 used these buffers
+        if (busy[b]) {   // round r - 2 used these buffers
             if (hipEventSynchronize(c->rev[b]) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
             rc = check(b);
             if (rc) break;
         }
         sock_add(13, now_ns() - t0);
+        // ---- stage the round's payloads (packed, 16-byte aligned starts) ----
         t0 = now_ns();
         size_t at = 0;
         for (int i = 0; i < M; i++) {
-            const long long *o = &offs[(size_t)i * (nch + 1)];
-            for (int k = 0; k < nch; k++) {
-                const unsigned char *hp = (const unsigned char *)rb[i]->data + o[k];
+            const long long *o = &offs[(size_t)i * (maxf + 1)];
+            for (int q = 0; q < nf; q++) {
+                const unsigned char *hp = (const unsigned char *)rb[i]->data + o[q];
                 const int sz = (int)((uint32_t)hp[0] | ((uint32_t)hp[1] << 8) | ((uint32_t)hp[2] << 16) |
                                      ((uint32_t)hp[3] << 24));
                 memcpy(c->h_stage[b] + at, hp + 4, (size_t)sz);
-                c->h_poff[b][(size_t)i * nch + k] = (long long)at;
-                c->h_csz[b][(size_t)k * M + i] = sz;
+                c->h_poff[b][(size_t)i * nf + q] = (long long)at;
+                c->h_csz[b][(size_t)q * M + i] = sz;
                 at = (at + (size_t)sz + 15) & ~(size_t)15;
             }
-            APE_LZ4_rxbuf_consume(rb[i], (size_t)o[nch]);
+            APE_LZ4_rxbuf_consume(rb[i], (size_t)o[nf]);
             parsed[i] = 0;
         }
         sock_add(9, now_ns() - t0);
-        // ---- H2D, nch usingDict launches of M blocks, D2H into the caller's rows ----
+        // ---- H2D, k x nch usingDict launches of M blocks, D2H into the caller's rows ----
+        if (chain_slide(c->rxwin, c->W, M, c->rxpos, (size_t)k * c->msg, c->rst) != hipSuccess) {
+            rc = APE_LZ4_GPU_ELAUNCH;
+            break;
+        }
         hipError_t e = hipMemcpyAsync(c->rstage[b], c->h_stage[b], at + 16, hipMemcpyHostToDevice, c->rst);
         if (e == hipSuccess)
-            e = hipMemcpyAsync(c->rpoff[b], c->h_poff[b], (size_t)nt * sizeof(long long), hipMemcpyHostToDevice, c->rst);
+            e = hipMemcpyAsync(c->rpoff[b], c->h_poff[b], (size_t)ne * sizeof(long long), hipMemcpyHostToDevice, c->rst);
         if (e == hipSuccess)
-            e = hipMemcpyAsync(c->rcsz[b], c->h_csz[b], (size_t)nt * sizeof(int), hipMemcpyHostToDevice, c->rst);
+            e = hipMemcpyAsync(c->rcsz[b], c->h_csz[b], (size_t)ne * sizeof(int), hipMemcpyHostToDevice, c->rst);
         if (e != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
-        hipLaunchKernelGGL(chain_rx_setup, dim3((nt + 255) / 256), dim3(256), 0, c->rst, c->rstage[b],
-                           c->rpoff[b], c->rxwin, c->W, c->rxpos, c->msg, nch, M, c->rsrc, c->rdst,
+        hipLaunchKernelGGL(chain_rx_setup, dim3((ne + 255) / 256), dim3(256), 0, c->rst, c->rstage[b],
+                           c->rpoff[b], c->rxwin, c->W, c->rxpos, c->msg, nch, k, M, c->rsrc, c->rdst,
                            c->rcap, c->rdict, c->rdsz);
         if (hipGetLastError() != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
-        for (int k = 0; k < nch && rc == 0; k++) {
-            const size_t e0 = (size_t)k * M;
+        for (int q = 0; q < nf && rc == 0; q++) {
+            const size_t e0 = (size_t)q * M;
             rc = APE_LZ4_decompress_safe_usingDict_batch_dev(c->rsrc + e0, c->rcsz[b] + e0, c->rdst + e0,
                                                              c->rcap + e0, c->rdict + e0, c->rdsz + e0,
                                                              c->rres[b] + e0, M, c->rst);
         }
         if (rc) break;
-        e = hipMemcpy2DAsync(h_out + (size_t)m * M * out_stride, out_stride, c->rxwin + c->rxpos, c->W,
-                             (size_t)c->msg, (size_t)M, hipMemcpyDeviceToHost, c->rst);
+        for (int mm = 0; mm < k && e == hipSuccess; mm++)
+            e = hipMemcpy2DAsync(h_out + (size_t)(r * c->K + mm) * M * out_stride, out_stride,
+                                 c->rxwin + c->rxpos + (size_t)mm * c->msg, c->W, (size_t)c->msg,
+                                 (size_t)M, hipMemcpyDeviceToHost, c->rst);
         if (e == hipSuccess)
-            e = hipMemcpyAsync(c->h_res[b], c->rres[b], (size_t)nt * sizeof(int), hipMemcpyDeviceToHost, c->rst);
+            e = hipMemcpyAsync(c->h_res[b], c->rres[b], (size_t)ne * sizeof(int), hipMemcpyDeviceToHost, c->rst);
         if (e == hipSuccess) e = hipEventRecord(c->rev[b], c->rst);
         if (e != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
         busy[b] = true;
-        bround[b] = m;
+        bk[b] = k;
         sock_add(14, 1);
-        c->rxpos += (uint32_t)c->msg;
-        if (chain_slide(c->rxwin, c->W, M, c->rxpos, c->msg, c->rst) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        c->rxpos += (uint32_t)(k * c->msg);
     }
     // drain every round in flight, whatever rc is, before the buffers are reused
     for (int b2 = 0; b2 < 2; b2++) {
-        const int b = (nmsg + b2) & 1;   // the older round first
+        const int b = (nr + b2) & 1;   // the older round first
         if (!busy[b]) continue;
         if (hipEventSynchronize(c->rev[b]) != hipSuccess) {
             if (rc == 0) rc = APE_LZ4_GPU_ELAUNCH;

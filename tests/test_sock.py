@@ -345,11 +345,14 @@ def _drain(sock):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("msg_len,nmsg", [(65536, 6), (25576, 5)])
-def test_chain_gpu_tx_decoded_by_reference(cuda, product, msg_len, nmsg):
+@pytest.mark.parametrize("msg_len,nmsg,per_round", [(65536, 6, 0), (65536, 7, 2), (25576, 5, 3)])
+def test_chain_gpu_tx_decoded_by_reference(cuda, product, monkeypatch, msg_len, nmsg, per_round):
     """GPU chain_send writes the reference's wire format: the reference's own
     decompress_safe_continue + 64 KiB dictionary ring (ape_socket.c:1386-1421) restores every
-    message of every connection, across window slides (6 x 64 KiB > 2 x 64 KiB + 64 KiB)."""
+    message of every connection -- in one round, and in rounds of 2-3 messages (window slides,
+    a partial last round)."""
+    if per_round:
+        monkeypatch.setenv("APE_LZ4_CHAIN_ROUND", str(per_round))
     nconn = 5
     peer = _ref_peer()
     msgs = _chain_msgs(cuda, product, nmsg, nconn, msg_len, seed=msg_len)
@@ -394,11 +397,16 @@ def test_chain_gpu_tx_decoded_by_reference(cuda, product, msg_len, nmsg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("msg_len,nmsg,pieces", [(65536, 6, False), (25576, 4, True)])
-def test_chain_reference_tx_decoded_by_gpu(cuda, product, msg_len, nmsg, pieces):
+@pytest.mark.parametrize("msg_len,nmsg,pieces,per_round", [(65536, 6, False, 0), (65536, 7, False, 2),
+                                                           (25576, 4, True, 3)])
+def test_chain_reference_tx_decoded_by_gpu(cuda, product, monkeypatch, msg_len, nmsg, pieces,
+                                           per_round):
     """GPU chain_recv reads the reference's wire format: frames from the reference's own
-    compress_fast_continue + saveDict (ape_socket.c:811-871) decode bit-exactly, also when the
-    sender writes them in 1-7-byte and random pieces (every header split: the K7 parser)."""
+    compress_fast_continue + saveDict (ape_socket.c:811-871) decode bit-exactly -- in one round
+    and in rounds of 2-3 messages (window slides, a partial last round) -- also when the sender
+    writes them in 1-7-byte and random pieces (every header split: the K7 parser)."""
+    if per_round:
+        monkeypatch.setenv("APE_LZ4_CHAIN_ROUND", str(per_round))
     nconn = 4
     peer = _ref_peer()
     msgs = _chain_msgs(cuda, product, nmsg, nconn, msg_len, seed=msg_len + 1)
