@@ -603,15 +603,7 @@ def sock_leg(args):
     split = amd.socket_stats(reset=True)
     ok = got == nb and bool((res == n).all()) and bool(torch.equal(h_dst, h_src))
     # the same wire bytes through the same kind of connection without the codec
-    ceiling = None
-    try:
-        cb = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
-        cb.sock_ceiling.argtypes = [C.c_longlong, C.c_int, C.POINTER(C.c_double)]
-        o2 = (C.c_double * 2)()
-        if cb.sock_ceiling(int(wire), 4 << 20, o2) == 0:
-            ceiling = round(o2[1] / o2[0] / 1e9, 3)
-    except OSError:
-        pass
+    ceiling, ceiling_cold = sock_ceilings(int(wire))
     cpu = None if args.no_cpu_baseline else cpu_sock_baseline(n)
     line = {
         "metric": "LZ4 GiB/s through a loopback TCP socket (GPU encode -> frames -> socket -> "
@@ -623,17 +615,38 @@ def sock_leg(args):
                                "per GPU batch" % (nb, n >> 10, batch)},
         "wall_s": round(wall, 3), "wire_bytes": int(wire), "ratio": round(nb * n / (wire - 4 * nb), 4),
         "wire_GBps": round(wire / wall / 1e9, 3), "verified": ok,
-        "ceiling_GBps": ceiling,
-        "ceiling": "plain bytes over one 127.0.0.1 TCP connection, 4 MiB write()s, no codec "
-                   "(oracle/cpu_bench.c sock_ceiling), same wire bytes",
+        "ceiling_GBps": ceiling, "ceiling_cold_GBps": ceiling_cold,
+        "wire_frac_of_ceiling": round(wire / wall / 1e9 / ceiling, 3) if ceiling else None,
+        "wire_frac_of_cold_ceiling": round(wire / wall / 1e9 / ceiling_cold, 3) if ceiling_cold else None,
+        "ceiling": "plain bytes over one 127.0.0.1 TCP connection, 4 MiB write()s / read()s, no "
+                   "codec, same wire bytes (oracle/cpu_bench.c sock_ceiling_buf): ceiling_GBps "
+                   "with one 4 MiB buffer per side (cache-hot), ceiling_cold_GBps walking 1 GiB "
+                   "buffers (every syscall copies cache-cold memory, as the codec path's do: its "
+                   "frames arrive by DMA and its receive buffer is read by DMA)",
         "split_ms": split,
         "split_note": "GPU phases from timing events per batch (they overlap each other and "
                       "the socket I/O: double-buffered); write/read = time in the syscalls; "
                       "gpu_wait = host blocked on the GPU",
         "cpu_baseline": cpu,
     }
-    line["bound"] = ("socket" if ceiling and line["wire_GBps"] >= 0.8 * ceiling else "pipeline")
+    line["bound"] = ("socket" if ceiling_cold and line["wire_GBps"] >= 0.8 * ceiling_cold
+                     else "pipeline")
     return line
+
+
+def sock_ceilings(nbytes):
+    """(hot, cold) plain-bytes loopback rates in GB/s for nbytes (oracle/cpu_bench.c)."""
+    try:
+        cb = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
+        cb.sock_ceiling_buf.argtypes = [C.c_longlong, C.c_int, C.c_longlong, C.POINTER(C.c_double)]
+        o2 = (C.c_double * 2)()
+        res = []
+        for buf in (4 << 20, 1 << 30):
+            res.append(round(o2[1] / o2[0] / 1e9, 3)
+                       if cb.sock_ceiling_buf(nbytes, 4 << 20, buf, o2) == 0 else None)
+        return tuple(res)
+    except OSError:
+        return None, None
 
 
 def sock_chained_leg(args):
@@ -653,6 +666,11 @@ def sock_chained_leg(args):
 
     import libapenetwork_amd as amd
 
+    import resource
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    want = 4 * args.chain_conns + 256        # GPU and reference legs: 2 fds per connection each
+    if soft < want:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (min(want, hard), hard))
     torch.cuda.set_device(0)
     if amd.gpu_init() != 0:
         raise SystemExit("GPU codec unavailable: %s" % amd.gpu_last_error())
@@ -722,33 +740,26 @@ def sock_chained_leg(args):
     cpu = None
     if not args.no_cpu_baseline:
         lib = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
-        lib.cpu_sock_run.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int,
-                                     C.POINTER(C.c_double)]
+        lib.cpu_sock_run2.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_int, C.POINTER(C.c_double)]
         ref = os.path.join(ROOT, "oracle", "_ref", "libape_lz4_ref.so")
         path, prefix, kind = ((ref, b"APE_LZ4_", "reference") if os.path.exists(ref) else
                               (os.path.join(ROOT, "oracle", "liblz4_oracle.so"), b"orc_", "port"))
         o = (C.c_double * 4)()
-        cm = min(M, 128)
-        cmsg = max(8, args.chain_cpu_bytes // (cm * n))
+        cmsg = max(4, args.chain_cpu_bytes // (M * n))
         usable, cores = host_cores()
-        if lib.cpu_sock_run(path.encode(), prefix, cm, n, cmsg, 1, o) == 0 and o[3] == 0:
+        if lib.cpu_sock_run2(path.encode(), prefix, M, n, cmsg, 1, usable, o) == 0 and o[3] == 0:
             cpu = {"value": round(o[1] / o[0] / GIB, 3), "unit": "GiB/s", "cores": usable,
-                   "kind": kind, "connections": cm, "threads": 2 * cm,
+                   "kind": kind, "connections": M, "threads": 2 * min(usable, M),
                    "wire_GBps": round(o[2] / o[0] / 1e9, 3), "seconds": round(o[0], 2),
-                   "sample": "%d connections x %d x 64 KiB App. C messages, the reference socket "
-                             "codec (compress_fast_continue + saveDict / decompress_safe_continue "
-                             "+ 64 KiB ring), one TX and one RX thread per connection on %d usable "
-                             "cores; generated before and compared after the clock" % (cm, cmsg, usable),
+                   "sample": "the same %d connections x %d x 64 KiB App. C messages through the "
+                             "reference socket codec (compress_fast_continue + saveDict / "
+                             "decompress_safe_continue + 64 KiB ring), an event loop per usable "
+                             "core: %d TX and %d RX threads, each serving every %d-th connection "
+                             "(poll); generated before and compared after the clock" % (
+                                 M, cmsg, min(usable, M), min(usable, M), min(usable, M)),
                    "host": cores}
-    ceiling = None
-    try:
-        cb = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
-        cb.sock_ceiling.argtypes = [C.c_longlong, C.c_int, C.POINTER(C.c_double)]
-        o2 = (C.c_double * 2)()
-        if cb.sock_ceiling(int(wire), 4 << 20, o2) == 0:
-            ceiling = round(o2[1] / o2[0] / 1e9, 3)
-    except OSError:
-        pass
+    ceiling, ceiling_cold = sock_ceilings(int(wire))
     return {
         "metric": "LZ4 GiB/s, the reference socket wire format (chained 8 KiB blocks) through the "
                   "GPU over %d loopback TCP connections" % M,
@@ -759,9 +770,9 @@ def sock_chained_leg(args):
                                "chunks, [int32 size][block] frames" % (M, nmsg, payload / GIB)},
         "wall_s": round(wall, 3), "wire_bytes": int(wire), "ratio": round(payload / (wire - 4 * nmsg * M * 8), 4),
         "wire_GBps": round(wire / wall / 1e9, 3), "verified": ok,
-        "ceiling_GBps": ceiling,
-        "ceiling": "plain bytes over one 127.0.0.1 TCP connection, 4 MiB write()s (sock_ceiling), "
-                   "same wire bytes",
+        "ceiling_GBps": ceiling, "ceiling_cold_GBps": ceiling_cold,
+        "ceiling": "plain bytes over one 127.0.0.1 TCP connection, 4 MiB write()s (sock_ceiling_buf), "
+                   "same wire bytes; hot: one 4 MiB buffer per side, cold: 1 GiB buffers",
         "split_ms": {k: v for k, v in split.items() if k in (
             "tx_write_ms", "tx_gpu_wait_ms", "tx_batches", "tx_total_ms", "rx_total_ms",
             "rx_read_ms", "rx_parse_ms", "rx_gpu_wait_ms", "rx_batches")},
@@ -977,9 +988,9 @@ def main():
     ap.add_argument("--sock-batch", type=int, default=2048)
     ap.add_argument("--sock-chained", action="store_true",
                     help="the reference wire format (chained 8 KiB blocks) over many sockets")
-    ap.add_argument("--chain-conns", type=int, default=128)
-    ap.add_argument("--chain-msgs", type=int, default=128,
-                    help="64 KiB messages per connection (128 x 128 x 64 KiB = 1 GiB)")
+    ap.add_argument("--chain-conns", type=int, default=512)
+    ap.add_argument("--chain-msgs", type=int, default=32,
+                    help="64 KiB messages per connection (512 x 32 x 64 KiB = 1 GiB)")
     ap.add_argument("--chain-cpu-bytes", type=int, default=1 << 30,
                     help="payload of the reference socket-codec baseline run")
     args = ap.parse_args()

@@ -129,8 +129,12 @@ constexpr uint32_t kFetchAt = 48, kEmitAll = 80, kChunkRecs = 64u / 4u;
 static_assert((kQ & (kQ - 1u)) == 0u, "record ring indexed by & (kQ - 1)");
 static_assert(kEmitAll - 1u + 2u * kChunkRecs <= kQ, "walker -> emitter record ring overflow");
 static_assert(kFetchAt < kEmitAll, "a fetch precedes emit_all");
+// acceleration > 1 keeps the in-chunk candidate: the reference's table holds every earlier
+// probe with no lag, the GPU's lags a chunk or two, and at sparse probes L is what finds the
+// near matches (ratio within 1 % of the reference at a = 2, 4, 8 with it, 2.5-2.7 % below
+// without: DESIGN.md 3.1); 0 = the faster search without it
 #ifndef APE_LZ4_ACC_L
-#define APE_LZ4_ACC_L 0              // acceleration > 1 keeps the in-chunk candidate
+#define APE_LZ4_ACC_L 1
 #endif
 #ifndef APE_EMIT_EVERY
 #define APE_EMIT_EVERY 8             // emitter: a batch every this many steps (at most)
@@ -930,7 +934,24 @@ __device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk 
     const uint32_t end = mem ? p + O.Lf : 0u;
     const uint32_t imax = wave_incl_max(end);
     const uint32_t pm = umax(wave_shr1(imax, 0u), anchor0);
-    const uint32_t bk = umin((O.iv.x >> 8) & 7u, p - pm);
+    uint32_t bk = umin((O.iv.x >> 8) & 7u, p - pm);
+    if (ACC) {
+        // acceleration probes every stride-th position, so a match found at a probe often
+        // starts further back than the 4 bytes C1 measured: the reference's catch-up
+        // (:623-627) is unbounded -- continue it byte by byte here (up to 16 more bytes; the
+        // ACC path only), stopping at the pending literals' start and the window start
+        const uint32_t c = p - (O.iv.y & 0xFFFFu);
+        const uint32_t room = umin(p - pm, c);
+        if (mem && bk == 4u && room > 4u) {
+            const uint32_t lim = umin(room - 4u, 16u);
+            uint32_t more = 0;
+            for (uint32_t t = 1; t <= lim; t++) {
+                if (B.in[p - 4u - t] != B.in[c - 4u - t]) break;
+                more = t;
+            }
+            bk += more;
+        }
+    }
     O.m_back = bk;
     O.m_len = O.Lf + bk;
     O.an = pm;
@@ -1460,8 +1481,7 @@ lz4_encode_kernel(BlockArgs a) {
     B.n = D + nr;
     B.nr = (uint32_t)nr;
     B.k0 = D / 64;
-    // compress_fast's acceleration (:789-808) trades ratio for speed; here that is the
-    // in-chunk candidate (-11 % encode time, ratio -1.7 % on App. C data)
+    // compress_fast's acceleration (:789-808): the reference's probe pattern (walk_chain)
 #ifdef APE_EXP_NOL
     B.noL = true;   // diagnostic: no in-chunk candidate search (its LDS atomics)
 #else

@@ -259,6 +259,12 @@ void APE_LZ4_rxbuf_free(APE_LZ4_rxbuf *b) {
 // TX: compress nblocks blocks of block_size bytes (block i at h_src + i*src_stride) on the
 // current device, `batch` at a time, and write the framed stream to fd.  Returns the
 // bytes written, or a negative APE_LZ4_GPU_E* code.
+// The frame-pack kernel stores each batch's frames straight into a pinned, device-mapped
+// send buffer (zero-copy over PCIe), so no D2H copy waits for the batch's size: the host
+// only waits for the batch's kernels, then write()s the buffer while the GPU encodes and
+// packs the next ones into the other buffers.  kSlots batch slots: the
+// H2D of one batch, the kernels of another and the write() of a third overlap.
+constexpr int kSlots = 3;
 long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_stride,
                                      int block_size, int nblocks, int batch) {
     if (fd < 0 || !h_src || block_size <= 0 || block_size > kMaxBlock || nblocks < 0 || batch <= 0 ||
@@ -267,22 +273,21 @@ long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_strid
     int rc = APE_LZ4_gpu_init();
     if (rc) return rc;
     const size_t slot = up16((size_t)bound_of(block_size));
-    Dev d[2];
-    char *hf[2] = {nullptr, nullptr};
-    long long *htot[2] = {nullptr, nullptr};
+    Dev d[kSlots];
+    char *hf[kSlots] = {}, *df[kSlots] = {};   // pinned send buffers: host / device views
+    long long *htot[kSlots] = {};
     long long sent = 0;
-    int nb[2] = {0, 0};
     const int nbat = (nblocks + batch - 1) / batch;
-    for (int i = 0; i < 2 && rc == 0; i++) {
+    for (int i = 0; i < kSlots && rc == 0; i++) {
         if (dev_alloc(d[i], batch, block_size, true) != 0 ||
             hipHostMalloc((void **)&hf[i], (size_t)batch * (slot + 4) + 64, hipHostMallocDefault) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&df[i], hf[i], 0) != hipSuccess ||
             hipHostMalloc((void **)&htot[i], sizeof(long long), hipHostMallocDefault) != hipSuccess)
             rc = APE_LZ4_GPU_ENOMEM;
     }
     auto launch = [&](int c) -> int {
-        Dev &D = d[c & 1];
+        Dev &D = d[c % kSlots];
         const int k = nblocks - c * batch < batch ? nblocks - c * batch : batch;
-        nb[c & 1] = k;
         const char *src = h_src + (size_t)c * batch * src_stride;
         (void)hipEventRecord(D.tev[0], D.st);
         hipError_t e = hipMemcpy2DAsync(D.src, (size_t)block_size, src, src_stride, (size_t)block_size,
@@ -292,42 +297,40 @@ long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_strid
         int r = APE_LZ4_compress_batch_strided_dev(D.src, (size_t)block_size, D.sizes, D.comp, slot,
                                                    nullptr, D.csz, k, D.st);
         if (r == 0) r = APE_LZ4_frame_offsets_dev(D.csz, D.off, D.scratch, k, D.st);
-        if (r == 0) r = APE_LZ4_frame_pack_strided_dev(D.comp, slot, D.csz, D.off, D.frames, k, D.st);
         if (r) return r;
         (void)hipEventRecord(D.tev[2], D.st);
-        e = hipMemcpyAsync(htot[c & 1], D.off + k, sizeof(long long), hipMemcpyDeviceToHost, D.st);
+        r = APE_LZ4_frame_pack_strided_dev(D.comp, slot, D.csz, D.off, df[c % kSlots], k, D.st);
+        if (r) return r;
+        (void)hipEventRecord(D.tev[3], D.st);
+        e = hipMemcpyAsync(htot[c % kSlots], D.off + k, sizeof(long long), hipMemcpyDeviceToHost, D.st);
         if (e == hipSuccess) e = hipEventRecord(D.ev, D.st);
         return e == hipSuccess ? 0 : APE_LZ4_GPU_ELAUNCH;
     };
     const long long ttx = now_ns();
-    if (rc == 0 && nbat > 0) rc = launch(0);
+    for (int c = 0; c < kSlots - 1 && c < nbat && rc == 0; c++) rc = launch(c);
     for (int c = 0; c < nbat && rc == 0; c++) {
-        Dev &D = d[c & 1];
+        Dev &D = d[c % kSlots];
         long long t0 = now_ns();
+        // the batch's kernels (frames already in hf) and its size
         if (hipEventSynchronize(D.ev) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
-        const long long tot = *htot[c & 1];
-        (void)hipEventRecord(D.tev[3], D.st);
-        if (hipMemcpyAsync(hf[c & 1], D.frames, (size_t)tot, hipMemcpyDeviceToHost, D.st) != hipSuccess ||
-            hipEventRecord(D.tev[4], D.st) != hipSuccess || hipStreamSynchronize(D.st) != hipSuccess) {
-            rc = APE_LZ4_GPU_ELAUNCH;
-            break;
-        }
+        const long long tot = *htot[c % kSlots];
         long long t1 = now_ns();
         sock_add(4, t1 - t0);
         sock_add(0, ev_ns(D.tev[0], D.tev[1]));
         sock_add(1, ev_ns(D.tev[1], D.tev[2]));
-        sock_add(2, ev_ns(D.tev[3], D.tev[4]));
+        sock_add(2, ev_ns(D.tev[2], D.tev[3]));   // the pack: frames over PCIe into hf
         sock_add(5, 1);
-        if (c + 1 < nbat) rc = launch(c + 1);   // the next batch's GPU work under this write
+        // batch c + kSlots - 1 into the slot batch c - 1 used (its write() is done)
+        if (c + kSlots - 1 < nbat) rc = launch(c + kSlots - 1);
         if (rc) break;
         t0 = now_ns();
-        const long long w = write_all(fd, hf[c & 1], (size_t)tot);
+        const long long w = write_all(fd, hf[c % kSlots], (size_t)tot);
         sock_add(3, now_ns() - t0);
         if (w < 0) { rc = APE_LZ4_GPU_EINVAL; break; }
         sent += w;
     }
     sock_add(6, now_ns() - ttx);
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < kSlots; i++) {
         dev_free(d[i]);
         if (hf[i]) (void)hipHostFree(hf[i]);
         if (htot[i]) (void)hipHostFree(htot[i]);
@@ -349,13 +352,14 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
     if (rc) return rc;
     const int maxc = bound_of(block_size);
     const size_t chunk = 4u << 20;   // read() granularity
-    Dev d[2];
-    APE_LZ4_rxbuf *rb[2] = {APE_LZ4_rxbuf_new(4u << 20), APE_LZ4_rxbuf_new(4u << 20)};
-    long long *hoff[2] = {nullptr, nullptr};
-    bool busy[2] = {false, false};
-    long long base[2] = {0, 0};   // first block of the batch in flight on d[i]
-    int cnt[2] = {0, 0};          // ... and its block count
-    for (int i = 0; i < 2 && rc == 0; i++) {
+    Dev d[kSlots];
+    APE_LZ4_rxbuf *rb[kSlots];
+    long long *hoff[kSlots] = {};
+    bool busy[kSlots] = {};
+    long long base[kSlots] = {};  // first block of the batch in flight on d[i]
+    int cnt[kSlots] = {};         // ... and its block count
+    for (int i = 0; i < kSlots; i++) rb[i] = APE_LZ4_rxbuf_new(4u << 20);
+    for (int i = 0; i < kSlots && rc == 0; i++) {
         if (!rb[i] || dev_alloc(d[i], batch, block_size, false) != 0 ||
             hipHostMalloc((void **)&hoff[i], ((size_t)batch + 1) * sizeof(long long),
                           hipHostMallocDefault) != hipSuccess)
@@ -391,8 +395,9 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
             b->used += (size_t)r;
             continue;
         }
-        // a full batch: hand this buffer to the GPU, continue receiving in the other one
-        const int nxt = cur ^ 1;
+        // a full batch: hand this buffer to the GPU, continue receiving in the next one (free
+        // once the batch kSlots - 1 back has finished: kSlots - 1 batches stay in flight)
+        const int nxt = (cur + 1) % kSlots;
         if (busy[nxt]) {
             t0 = now_ns();
             if (hipStreamSynchronize(d[nxt].st) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
@@ -438,7 +443,7 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
         parsed = 0;
     }
     sock_add(7, now_ns() - trx);
-    for (int i = 0; i < 2; i++) {   // drain every batch in flight, whatever rc is
+    for (int i = 0; i < kSlots; i++) {   // drain every batch in flight, whatever rc is
         if (!busy[i]) continue;
         if (hipStreamSynchronize(d[i].st) != hipSuccess) {
             if (rc == 0) rc = APE_LZ4_GPU_ELAUNCH;   // its results never reached h_result
@@ -452,7 +457,7 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
             memcpy(h_result + base[i], d[i].hres, (size_t)cnt[i] * sizeof(int));
         }
     }
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < kSlots; i++) {
         dev_free(d[i]);
         APE_LZ4_rxbuf_free(rb[i]);
         if (hoff[i]) (void)hipHostFree(hoff[i]);
@@ -534,13 +539,14 @@ struct APE_LZ4_chain {
     // TX (one thread): device window, compressed slots, frames, pointer arrays
     hipStream_t tst = nullptr;
     hipEvent_t tev[2] = {nullptr, nullptr};
-    char *txwin = nullptr, *slots = nullptr, *frames = nullptr;
+    char *txwin = nullptr, *slots = nullptr;
     int *csz = nullptr, *size = nullptr, *pre = nullptr, *cap = nullptr;
     const char **src = nullptr;
     char **dst = nullptr;
     long long *off = nullptr;
     void *scratch = nullptr;
-    char *h_frames = nullptr;
+    char *h_frames[2] = {nullptr, nullptr};   // pinned; the pack kernel writes them (zero-copy)
+    char *d_hframes[2] = {nullptr, nullptr};  // their device-mapped addresses
     long long *h_off[2] = {nullptr, nullptr};
     uint32_t txpos = 0;
     // RX (one thread): device window, staged payloads, pointer arrays, results
@@ -562,7 +568,7 @@ namespace {
 void chain_release(APE_LZ4_chain *c) {
     if (c->tst) (void)hipStreamSynchronize(c->tst);
     if (c->rst) (void)hipStreamSynchronize(c->rst);
-    for (void *p : {(void *)c->txwin, (void *)c->slots, (void *)c->frames, (void *)c->csz,
+    for (void *p : {(void *)c->txwin, (void *)c->slots, (void *)c->csz,
                     (void *)c->size, (void *)c->pre, (void *)c->cap, (void *)c->src, (void *)c->dst,
                     (void *)c->off, c->scratch, (void *)c->rxwin, (void *)c->rstage[0],
                     (void *)c->rstage[1], (void *)c->rpoff[0], (void *)c->rpoff[1],
@@ -570,7 +576,7 @@ void chain_release(APE_LZ4_chain *c) {
                     (void *)c->rres[0], (void *)c->rres[1], (void *)c->rsrc, (void *)c->rdict,
                     (void *)c->rdst})
         if (p) (void)hipFree(p);
-    for (void *p : {(void *)c->h_frames, (void *)c->h_off[0], (void *)c->h_off[1],
+    for (void *p : {(void *)c->h_frames[0], (void *)c->h_frames[1], (void *)c->h_off[0], (void *)c->h_off[1],
                     (void *)c->h_stage[0], (void *)c->h_stage[1], (void *)c->h_poff[0],
                     (void *)c->h_poff[1], (void *)c->h_csz[0], (void *)c->h_csz[1],
                     (void *)c->h_res[0], (void *)c->h_res[1]})
@@ -628,14 +634,16 @@ APE_LZ4_chain *APE_LZ4_chain_new(int nconn, int msg_len) {
     for (int b = 0; b < 2 && ok; b++)
         ok = hipEventCreateWithFlags(&c->tev[b], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->rev[b], hipEventDisableTiming) == hipSuccess &&
-             halloc(c->h_off[b], nt + 1) && dalloc(c->rstage[b], fr) && dalloc(c->rpoff[b], nt) &&
+             halloc(c->h_off[b], nt + 1) && halloc(c->h_frames[b], fr) &&
+             hipHostGetDevicePointer((void **)&c->d_hframes[b], c->h_frames[b], 0) == hipSuccess &&
+             dalloc(c->rstage[b], fr) && dalloc(c->rpoff[b], nt) &&
              dalloc(c->rcsz[b], nt) && dalloc(c->rres[b], nt) && halloc(c->h_stage[b], fr) &&
              halloc(c->h_poff[b], nt) && halloc(c->h_csz[b], nt) && halloc(c->h_res[b], nt);
     ok = ok && dalloc(c->txwin, (size_t)nconn * c->W) && dalloc(c->slots, nt * kChunkSlot) &&
-         dalloc(c->frames, fr) && dalloc(c->csz, nt) && dalloc(c->size, nt) && dalloc(c->pre, nt) &&
+         dalloc(c->csz, nt) && dalloc(c->size, nt) && dalloc(c->pre, nt) &&
          dalloc(c->cap, nt) && dalloc(c->src, nt) && dalloc(c->dst, nt) && dalloc(c->off, nt + 1) &&
          hipMalloc(&c->scratch, APE_LZ4_frame_scratch_size(c->nt) + 16) == hipSuccess &&
-         halloc(c->h_frames, fr) && dalloc(c->rxwin, (size_t)nconn * c->W) && dalloc(c->rcap, nt) &&
+         dalloc(c->rxwin, (size_t)nconn * c->W) && dalloc(c->rcap, nt) &&
          dalloc(c->rdsz, nt) && dalloc(c->rsrc, nt) && dalloc(c->rdict, nt) && dalloc(c->rdst, nt);
     if (!ok) {
         chain_release(c);
@@ -676,7 +684,8 @@ long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msg
         int e = APE_LZ4_compress_withPrefix_batch_dev(c->src, c->size, c->pre, c->dst, c->cap,
                                                       c->csz, nt, c->tst);
         if (e == 0) e = APE_LZ4_frame_offsets_dev(c->csz, c->off, c->scratch, nt, c->tst);
-        if (e == 0) e = APE_LZ4_frame_pack_strided_dev(c->slots, kChunkSlot, c->csz, c->off, c->frames, nt, c->tst);
+        // frames straight into the pinned send buffer of this round (zero-copy)
+        if (e == 0) e = APE_LZ4_frame_pack_strided_dev(c->slots, kChunkSlot, c->csz, c->off, c->d_hframes[b], nt, c->tst);
         if (e) return e;
         if (hipMemcpyAsync(c->h_off[b], c->off, ((size_t)nt + 1) * sizeof(long long),
                            hipMemcpyDeviceToHost, c->tst) != hipSuccess ||
@@ -695,11 +704,6 @@ long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msg
         const long long tot = off[nt];
         // a chunk that did not fit its bound is a codec failure (never for valid sizes)
         if (tot <= 4ll * nt) { rc = APE_LZ4_GPU_ELAUNCH; break; }
-        if (hipMemcpyAsync(c->h_frames, c->frames, (size_t)tot, hipMemcpyDeviceToHost, c->tst) != hipSuccess ||
-            hipStreamSynchronize(c->tst) != hipSuccess) {
-            rc = APE_LZ4_GPU_ELAUNCH;
-            break;
-        }
         sock_add(4, now_ns() - t0);
         sock_add(5, 1);
         if (r + 1 < nr) rc = launch(r + 1);   // the next round's GPU work under these writes
@@ -707,7 +711,7 @@ long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msg
         t0 = now_ns();
         for (int i = 0; i < M && rc == 0; i++) {   // connection i's frames of the round
             const long long a = off[(size_t)i * k * nch], e = off[(size_t)(i + 1) * k * nch];
-            const long long w = write_all(fds[i], c->h_frames + a, (size_t)(e - a));
+            const long long w = write_all(fds[i], c->h_frames[b] + a, (size_t)(e - a));
             if (w < 0) rc = APE_LZ4_GPU_EINVAL;
             else sent += w;
         }

@@ -366,15 +366,20 @@ void cpu_bench_free(void *h)
  *     frames [int32 size][block] (a split-safe parser: the reference's desyncs),
  *     decompress_safe_continue into an 8 KiB block, append it to the 64 KiB dictionary
  *     buffer (memmove when full, :1398-1413) and setStreamDecode on it (:1421).
- * One TX and one RX thread per connection; messages are the App. C blocks of
- * `msg` bytes (the benchmark's 64 KiB).  Timed region = the GPU leg's (bench.py sock_leg):
- * every message is generated before the clock starts and the delivered payload is compared
- * after it stops, so the clock holds only compress/frame/write and read/parse/decode/ring
- * work.  out: [0] seconds, [1] payload bytes, [2] wire bytes, [3] errors.
+ * Threads: nthr TX threads and nthr RX threads (nthr <= nconn), thread t serving the
+ * connections i = t, t + nthr, ... -- one connection per thread pair for nthr = nconn (the
+ * config 5 single connection), an event loop per core for many connections (a TX thread
+ * sends message m of each of its connections in turn; an RX thread polls its sockets).
+ * Messages are the App. C blocks of `msg` bytes (the benchmark's 64 KiB).  Timed region =
+ * the GPU leg's (bench.py sock_leg): every message is generated before the clock starts and
+ * the delivered payload is compared after it stops, so the clock holds only
+ * compress/frame/write and read/parse/decode/ring work.  out: [0] seconds, [1] payload
+ * bytes, [2] wire bytes, [3] errors.
  * --------------------------------------------------------------------------------- */
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -385,7 +390,7 @@ typedef int (*ssave_fn)(void *, char *, int);
 typedef int (*sdc_fn)(void *, const char *, char *, int, int);
 typedef int (*ssetd_fn)(void *, const char *, int);
 
-enum { SK_BLOCK = 8192, SK_DICT = 65536 };
+enum { SK_BLOCK = 8192, SK_DICT = 65536, SK_RBUF = 1 << 20 };
 
 typedef struct {
     smk_fn mk, mkd;
@@ -394,13 +399,24 @@ typedef struct {
     ssave_fn save;
     sdc_fn dc;
     ssetd_fn setd;
-    int fd_tx, fd_rx, msg, nmsg, kind, conn;
-    long long wire;
-    int bad;
-    uint8_t *src;   /* nmsg * msg bytes, generated before the clock starts */
-    uint8_t *dst;   /* nmsg * msg bytes, the delivered payload, compared after it stops */
-    long long delivered;
+} skfn_t;
+
+typedef struct {               /* one connection */
+    int fd_tx, fd_rx;
+    uint8_t *src;              /* nmsg * msg bytes, generated before the clock starts */
+    uint8_t *dst;              /* nmsg * msg bytes, the delivered payload */
+    long long delivered, wire;
+    void *st, *sd;             /* TX stream, RX stream decode */
+    char *dict_tx, *ring, *rbuf;
+    size_t used;
+    int dpos, eof, bad;
 } sconn_t;
+
+typedef struct {               /* one TX or RX thread */
+    const skfn_t *f;
+    sconn_t *cs;
+    int nconn, nthr, t, msg, nmsg;
+} sthr_t;
 
 static int sk_write_all(int fd, const char *p, size_t n)
 {
@@ -413,95 +429,113 @@ static int sk_write_all(int fd, const char *p, size_t n)
     return 0;
 }
 
-/* TX: compress + frame + write only (the messages are generated before
- * the clock, as the GPU leg's are) */
+/* TX: compress + frame + write only; message m of every connection of the thread in turn */
 static void *sk_tx(void *arg)
 {
-    sconn_t *c = (sconn_t *)arg;
+    sthr_t *T = (sthr_t *)arg;
     const int cap = SK_BLOCK + SK_BLOCK / 255 + 16;
-    char *frames = malloc((size_t)(c->msg / SK_BLOCK + 1) * (cap + 4));
-    char *dict = malloc(SK_DICT);
-    void *st = c->mk();
-    for (int m = 0; m < c->nmsg && st; m++) {
-        const uint8_t *msg = c->src + (size_t)m * c->msg;
-        int pos = 0;
-        for (int off = 0; off < c->msg; off += SK_BLOCK) {
-            const int len = c->msg - off < SK_BLOCK ? c->msg - off : SK_BLOCK;
-            const int r = c->cc(st, (const char *)msg + off, frames + pos + 4, len, cap, 1);
-            if (r <= 0) { c->bad++; break; }
-            memcpy(frames + pos, &r, 4);
-            pos += 4 + r;
+    char *frames = malloc((size_t)(T->msg / SK_BLOCK + 1) * (cap + 4));
+    for (int m = 0; m < T->nmsg && frames; m++) {
+        for (int i = T->t; i < T->nconn; i += T->nthr) {
+            sconn_t *c = &T->cs[i];
+            if (c->bad) continue;
+            const uint8_t *msg = c->src + (size_t)m * T->msg;
+            int pos = 0;
+            for (int off = 0; off < T->msg; off += SK_BLOCK) {
+                const int len = T->msg - off < SK_BLOCK ? T->msg - off : SK_BLOCK;
+                const int r = T->f->cc(c->st, (const char *)msg + off, frames + pos + 4, len, cap, 1);
+                if (r <= 0) { c->bad++; break; }
+                memcpy(frames + pos, &r, 4);
+                pos += 4 + r;
+            }
+            T->f->save(c->st, c->dict_tx, SK_DICT);
+            if (c->bad || sk_write_all(c->fd_tx, frames, (size_t)pos) != 0) { c->bad++; continue; }
+            c->wire += pos;
         }
-        c->save(st, dict, SK_DICT);
-        if (sk_write_all(c->fd_tx, frames, (size_t)pos) != 0) { c->bad++; break; }
-        c->wire += pos;
     }
-    shutdown(c->fd_tx, SHUT_WR);
-    if (st) c->fr(st);
-    free(frames); free(dict);
+    for (int i = T->t; i < T->nconn; i += T->nthr) shutdown(T->cs[i].fd_tx, SHUT_WR);
+    free(frames);
     return NULL;
 }
 
-/* RX: read + parse + decode + dictionary ring, each decoded block delivered to the
- * connection's payload buffer (the application's callback, :1423); compared after the clock */
+/* one connection's complete frames: decode, dictionary ring, deliver; 0 or -1 */
+static int sk_consume(const skfn_t *f, sconn_t *c, long long total)
+{
+    const int cap = SK_BLOCK + SK_BLOCK / 255 + 16;
+    char tmp[SK_BLOCK];
+    size_t p = 0;
+    while (c->used - p >= 4) {
+        int32_t sz;
+        memcpy(&sz, c->rbuf + p, 4);
+        if (sz <= 0 || sz > cap) return -1;
+        if (c->used - p - 4 < (size_t)sz) break;
+        const int rc = f->dc(c->sd, c->rbuf + p + 4, tmp, sz, SK_BLOCK);
+        if (rc <= 0) return -1;
+        if (c->dpos + rc > SK_DICT) {   /* :1398-1413 */
+            const int need = rc - (SK_DICT - c->dpos);
+            memmove(c->ring, c->ring + need, (size_t)(c->dpos - need));
+            memcpy(c->ring + c->dpos - need, tmp, (size_t)rc);
+            c->dpos = SK_DICT;
+        } else {
+            memcpy(c->ring + c->dpos, tmp, (size_t)rc);
+            c->dpos += rc;
+        }
+        f->setd(c->sd, c->ring, c->dpos);
+        if (c->delivered + rc > total) return -1;
+        memcpy(c->dst + c->delivered, tmp, (size_t)rc);   /* the application's callback, :1423 */
+        c->delivered += rc;
+        p += 4 + (size_t)sz;
+    }
+    memmove(c->rbuf, c->rbuf + p, c->used - p);
+    c->used -= p;
+    return 0;
+}
+
+/* RX: poll the thread's sockets, read + parse + decode + ring, until every one hits EOF */
 static void *sk_rx(void *arg)
 {
-    sconn_t *c = (sconn_t *)arg;
-    const int cap = SK_BLOCK + SK_BLOCK / 255 + 16;
-    const size_t bsz = 1u << 20;
-    const long long total = (long long)c->nmsg * c->msg;
-    char *buf = malloc(bsz);
-    char *dict = malloc(SK_DICT);
-    char tmp[SK_BLOCK];
-    void *sd = c->mkd();
-    size_t used = 0;
-    int dpos = 0;
+    sthr_t *T = (sthr_t *)arg;
+    const long long total = (long long)T->nmsg * T->msg;
+    const int mine = (T->nconn - T->t + T->nthr - 1) / T->nthr;
+    struct pollfd *pf = calloc((size_t)mine, sizeof *pf);
+    int *idx = calloc((size_t)mine, sizeof *idx);
+    if (!pf || !idx) { free(pf); free(idx); return NULL; }
     for (;;) {
-        ssize_t r = read(c->fd_rx, buf + used, bsz - used);
-        if (r < 0) { c->bad++; break; }
-        used += (size_t)r;
-        size_t p = 0;
-        while (used - p >= 4) {
-            int32_t sz;
-            memcpy(&sz, buf + p, 4);
-            if (sz <= 0 || sz > cap) { c->bad++; goto done; }
-            if (used - p - 4 < (size_t)sz) break;
-            const int rc = c->dc(sd, buf + p + 4, tmp, sz, SK_BLOCK);
-            if (rc <= 0) { c->bad++; goto done; }
-            if (dpos + rc > SK_DICT) {   /* :1398-1413 */
-                const int need = rc - (SK_DICT - dpos);
-                memmove(dict, dict + need, (size_t)(dpos - need));
-                memcpy(dict + dpos - need, tmp, (size_t)rc);
-                dpos = SK_DICT;
-            } else {
-                memcpy(dict + dpos, tmp, (size_t)rc);
-                dpos += rc;
-            }
-            c->setd(sd, dict, dpos);
-            if (c->delivered + rc > total) { c->bad++; goto done; }
-            memcpy(c->dst + c->delivered, tmp, (size_t)rc);
-            c->delivered += rc;
-            p += 4 + (size_t)sz;
+        int np = 0;
+        for (int i = T->t; i < T->nconn; i += T->nthr) {
+            if (T->cs[i].eof || T->cs[i].bad) continue;
+            pf[np].fd = T->cs[i].fd_rx;
+            pf[np].events = POLLIN;
+            pf[np].revents = 0;
+            idx[np++] = i;
         }
-        memmove(buf, buf + p, used - p);
-        used -= p;
-        if (r == 0) break;
+        if (np == 0) break;
+        if (np > 1 && poll(pf, (nfds_t)np, -1) < 0) continue;
+        for (int q = 0; q < np; q++) {
+            if (np > 1 && !(pf[q].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+            sconn_t *c = &T->cs[idx[q]];
+            ssize_t r = read(c->fd_rx, c->rbuf + c->used, SK_RBUF - c->used);
+            if (r < 0) { c->bad++; continue; }
+            if (r == 0) { c->eof = 1; continue; }
+            c->used += (size_t)r;
+            if (sk_consume(T->f, c, total) != 0) c->bad++;
+        }
     }
-done:
-    if (sd) c->frd(sd);
-    free(buf); free(dict);
+    free(pf);
+    free(idx);
     return NULL;
 }
 
-int cpu_sock_run(const char *lib, const char *prefix, int nconn, int msg, int nmsg, int kind,
-                 double *out)
+int cpu_sock_run2(const char *lib, const char *prefix, int nconn, int msg, int nmsg, int kind,
+                  int nthr, double *out)
 {
     char name[128];
     void *h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
-    if (!h || nconn < 1 || nconn > 128 || msg <= 0 || nmsg < 0) return -1;
-    sconn_t base;
-    memset(&base, 0, sizeof base);
-#define SYM(var, type, nm) snprintf(name, sizeof name, "%s" nm, prefix); base.var = (type)dlsym(h, name)
+    if (!h || nconn < 1 || nconn > 4096 || msg <= 0 || nmsg < 0 || nthr < 1) return -1;
+    if (nthr > nconn) nthr = nconn;
+    skfn_t f;
+    memset(&f, 0, sizeof f);
+#define SYM(var, type, nm) snprintf(name, sizeof name, "%s" nm, prefix); f.var = (type)dlsym(h, name)
     SYM(mk, smk_fn, "createStream");
     SYM(fr, sfree_fn, "freeStream");
     SYM(mkd, smk_fn, "createStreamDecode");
@@ -511,19 +545,23 @@ int cpu_sock_run(const char *lib, const char *prefix, int nconn, int msg, int nm
     SYM(dc, sdc_fn, "decompress_safe_continue");
     SYM(setd, ssetd_fn, "setStreamDecode");
 #undef SYM
-    if (!base.mk || !base.fr || !base.mkd || !base.frd || !base.cc || !base.save || !base.dc ||
-        !base.setd)
-        return -2;
+    if (!f.mk || !f.fr || !f.mkd || !f.frd || !f.cc || !f.save || !f.dc || !f.setd) return -2;
     sconn_t *cs = calloc((size_t)nconn, sizeof(sconn_t));
-    pthread_t *th = calloc((size_t)nconn * 2, sizeof(pthread_t));
-    int rc = 0;
+    sthr_t *ts = calloc((size_t)nthr * 2, sizeof(sthr_t));
+    pthread_t *th = calloc((size_t)nthr * 2, sizeof(pthread_t));
+    int rc = (cs && ts && th) ? 0 : -4;
     for (int i = 0; i < nconn && rc == 0; i++) {
-        cs[i] = base;
-        cs[i].msg = msg; cs[i].nmsg = nmsg; cs[i].kind = kind; cs[i].conn = i;
-        cs[i].src = malloc((size_t)nmsg * msg + 1);
-        cs[i].dst = malloc((size_t)nmsg * msg + 1);
-        if (!cs[i].src || !cs[i].dst) { rc = -4; break; }
-        synth_blocks(cs[i].src, msg, msg, (long long)i * nmsg, nmsg, kind);
+        sconn_t *c = &cs[i];
+        c->fd_tx = c->fd_rx = -1;
+        c->src = malloc((size_t)nmsg * msg + 1);
+        c->dst = malloc((size_t)nmsg * msg + 1);
+        c->dict_tx = malloc(SK_DICT);
+        c->ring = malloc(SK_DICT);
+        c->rbuf = malloc(SK_RBUF);
+        c->st = f.mk();
+        c->sd = f.mkd();
+        if (!c->src || !c->dst || !c->dict_tx || !c->ring || !c->rbuf || !c->st || !c->sd) { rc = -4; break; }
+        synth_blocks(c->src, msg, msg, (long long)i * nmsg, nmsg, kind);
         int ls = socket(AF_INET, SOCK_STREAM, 0), one = 1;
         struct sockaddr_in a;
         socklen_t al = sizeof a;
@@ -532,40 +570,52 @@ int cpu_sock_run(const char *lib, const char *prefix, int nconn, int msg, int nm
         a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
         setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
         if (ls < 0 || bind(ls, (struct sockaddr *)&a, sizeof a) || listen(ls, 1) ||
-            getsockname(ls, (struct sockaddr *)&a, &al)) { rc = -3; break; }
-        cs[i].fd_tx = socket(AF_INET, SOCK_STREAM, 0);
-        if (connect(cs[i].fd_tx, (struct sockaddr *)&a, sizeof a)) { rc = -3; break; }
-        cs[i].fd_rx = accept(ls, NULL, NULL);
+            getsockname(ls, (struct sockaddr *)&a, &al)) { if (ls >= 0) close(ls); rc = -3; break; }
+        c->fd_tx = socket(AF_INET, SOCK_STREAM, 0);
+        if (connect(c->fd_tx, (struct sockaddr *)&a, sizeof a)) { close(ls); rc = -3; break; }
+        c->fd_rx = accept(ls, NULL, NULL);
         close(ls);
-        if (cs[i].fd_rx < 0) { rc = -3; break; }
+        if (c->fd_rx < 0) { rc = -3; break; }
         int b = 4 << 20;
-        setsockopt(cs[i].fd_tx, SOL_SOCKET, SO_SNDBUF, &b, sizeof b);
-        setsockopt(cs[i].fd_rx, SOL_SOCKET, SO_RCVBUF, &b, sizeof b);
+        setsockopt(c->fd_tx, SOL_SOCKET, SO_SNDBUF, &b, sizeof b);
+        setsockopt(c->fd_rx, SOL_SOCKET, SO_RCVBUF, &b, sizeof b);
     }
-    const double t0 = now_s();
-    for (int i = 0; i < nconn && rc == 0; i++) {
-        pthread_create(&th[2 * i], NULL, sk_tx, &cs[i]);
-        pthread_create(&th[2 * i + 1], NULL, sk_rx, &cs[i]);
+    double t0 = 0, t1 = 0;
+    if (rc == 0) {
+        for (int t = 0; t < 2 * nthr; t++) {
+            ts[t].f = &f;
+            ts[t].cs = cs;
+            ts[t].nconn = nconn;
+            ts[t].nthr = nthr;
+            ts[t].t = t % nthr;
+            ts[t].msg = msg;
+            ts[t].nmsg = nmsg;
+        }
+        t0 = now_s();
+        for (int t = 0; t < nthr; t++) {
+            pthread_create(&th[2 * t], NULL, sk_tx, &ts[t]);
+            pthread_create(&th[2 * t + 1], NULL, sk_rx, &ts[nthr + t]);
+        }
+        for (int t = 0; t < 2 * nthr; t++) pthread_join(th[t], NULL);
+        t1 = now_s();
     }
     long long wire = 0;
     int bad = 0;
-    for (int i = 0; i < nconn && rc == 0; i++) {
-        pthread_join(th[2 * i], NULL);
-        pthread_join(th[2 * i + 1], NULL);
-        wire += cs[i].wire;
-        bad += cs[i].bad;
+    for (int i = 0; i < nconn && cs; i++) {
+        sconn_t *c = &cs[i];
+        if (rc == 0) {
+            wire += c->wire;
+            bad += c->bad;
+            if (c->delivered != (long long)nmsg * msg || memcmp(c->dst, c->src, (size_t)nmsg * msg) != 0)
+                bad++;
+        }
+        if (c->fd_tx >= 0) close(c->fd_tx);
+        if (c->fd_rx >= 0) close(c->fd_rx);
+        if (c->st) f.fr(c->st);
+        if (c->sd) f.frd(c->sd);
+        free(c->src); free(c->dst); free(c->dict_tx); free(c->ring); free(c->rbuf);
     }
-    const double t1 = now_s();
-    for (int i = 0; i < nconn; i++) {
-        if (rc == 0 && (cs[i].delivered != (long long)nmsg * msg ||
-                        memcmp(cs[i].dst, cs[i].src, (size_t)nmsg * msg) != 0))
-            bad++;
-        if (cs[i].fd_tx > 0) close(cs[i].fd_tx);
-        if (cs[i].fd_rx > 0) close(cs[i].fd_rx);
-        free(cs[i].src);
-        free(cs[i].dst);
-    }
-    free(cs); free(th);
+    free(cs); free(ts); free(th);
     if (rc) return rc;
     out[0] = t1 - t0;
     out[1] = (double)nconn * nmsg * msg;
@@ -574,28 +624,44 @@ int cpu_sock_run(const char *lib, const char *prefix, int nconn, int msg, int nm
     return 0;
 }
 
+/* one TX and one RX thread per connection (the round-3 interface) */
+int cpu_sock_run(const char *lib, const char *prefix, int nconn, int msg, int nmsg, int kind,
+                 double *out)
+{
+    return cpu_sock_run2(lib, prefix, nconn, msg, nmsg, kind, nconn, out);
+}
+
 /* sock_ceiling: plain bytes over one loopback TCP connection (no codec), `chunk`-byte
  * write()s from one thread and read()s into a buffer in another -- the ceiling of the
- * config 5 byte path.  out: [0] seconds, [1] bytes. */
-typedef struct { int fd; long long n; int chunk; } rawc_t;
+ * config 5 byte path.  sock_ceiling_buf: the same with the writer walking through a
+ * `buf_bytes` source buffer and the reader through a `buf_bytes` destination buffer: with
+ * 1 GiB buffers every syscall copies cache-cold memory, as the codec path's do (its frames
+ * arrive by DMA and its receive buffer is read by DMA; sock_ceiling's one 4 MiB buffer stays
+ * in the CPU caches).  out: [0] seconds, [1] bytes. */
+typedef struct { int fd; long long n; int chunk; const char *buf; size_t bsz; } rawc_t;
 
 static void *raw_tx(void *arg)
 {
     rawc_t *c = (rawc_t *)arg;
-    char *b = malloc((size_t)c->chunk);
-    memset(b, 0x5a, (size_t)c->chunk);
+    size_t pos = 0;
     for (long long left = c->n; left > 0;) {
         const int k = left < c->chunk ? (int)left : c->chunk;
-        if (sk_write_all(c->fd, b, (size_t)k)) break;
+        if (pos + (size_t)k > c->bsz) pos = 0;
+        if (sk_write_all(c->fd, c->buf + pos, (size_t)k)) break;
+        pos += (size_t)k;
         left -= k;
     }
     shutdown(c->fd, SHUT_WR);
-    free(b);
     return NULL;
 }
 
-int sock_ceiling(long long nbytes, int chunk, double *out)
+int sock_ceiling_buf(long long nbytes, int chunk, long long buf_bytes, double *out)
 {
+    if (chunk <= 0 || buf_bytes < chunk) return -1;
+    char *src = malloc((size_t)buf_bytes), *dst = malloc((size_t)buf_bytes);
+    if (!src || !dst) { free(src); free(dst); return -1; }
+    memset(src, 0x5a, (size_t)buf_bytes);
+    memset(dst, 0, (size_t)buf_bytes);
     int ls = socket(AF_INET, SOCK_STREAM, 0), one = 1, b = 4 << 20;
     struct sockaddr_in a;
     socklen_t al = sizeof a;
@@ -604,29 +670,37 @@ int sock_ceiling(long long nbytes, int chunk, double *out)
     a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
     setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
     if (ls < 0 || bind(ls, (struct sockaddr *)&a, sizeof a) || listen(ls, 1) ||
-        getsockname(ls, (struct sockaddr *)&a, &al)) return -1;
-    rawc_t c = {socket(AF_INET, SOCK_STREAM, 0), nbytes, chunk};
-    if (connect(c.fd, (struct sockaddr *)&a, sizeof a)) return -1;
+        getsockname(ls, (struct sockaddr *)&a, &al)) { free(src); free(dst); return -1; }
+    rawc_t c = {socket(AF_INET, SOCK_STREAM, 0), nbytes, chunk, src, (size_t)buf_bytes};
+    if (connect(c.fd, (struct sockaddr *)&a, sizeof a)) { free(src); free(dst); return -1; }
     const int rfd = accept(ls, NULL, NULL);
     close(ls);
     setsockopt(c.fd, SOL_SOCKET, SO_SNDBUF, &b, sizeof b);
     setsockopt(rfd, SOL_SOCKET, SO_RCVBUF, &b, sizeof b);
-    char *buf = malloc(1u << 20);
     pthread_t th;
     const double t0 = now_s();
     pthread_create(&th, NULL, raw_tx, &c);
     long long got = 0;
+    size_t pos = 0;
     for (;;) {
-        ssize_t r = read(rfd, buf, 1u << 20);
+        if (pos + (size_t)chunk > (size_t)buf_bytes) pos = 0;
+        ssize_t r = read(rfd, dst + pos, (size_t)chunk);
         if (r <= 0) break;
         got += r;
+        pos += (size_t)r;
     }
     pthread_join(th, NULL);
     const double t1 = now_s();
     close(c.fd);
     close(rfd);
-    free(buf);
+    free(src);
+    free(dst);
     out[0] = t1 - t0;
     out[1] = (double)got;
     return got == nbytes ? 0 : -2;
+}
+
+int sock_ceiling(long long nbytes, int chunk, double *out)
+{
+    return sock_ceiling_buf(nbytes, chunk, chunk, out);
 }
