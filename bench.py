@@ -989,8 +989,8 @@ def main():
     ap.add_argument("--sock-chained", action="store_true",
                     help="the reference wire format (chained 8 KiB blocks) over many sockets")
     ap.add_argument("--chain-conns", type=int, default=512)
-    ap.add_argument("--chain-msgs", type=int, default=32,
-                    help="64 KiB messages per connection (512 x 32 x 64 KiB = 1 GiB)")
+    ap.add_argument("--chain-msgs", type=int, default=64,
+                    help="64 KiB messages per connection (512 x 64 x 64 KiB = 2 GiB)")
     ap.add_argument("--chain-cpu-bytes", type=int, default=1 << 30,
                     help="payload of the reference socket-codec baseline run")
     args = ap.parse_args()

@@ -24,6 +24,7 @@
 //     (a caller runs TX and RX on their own threads, as the loopback benchmark does).
 #include <errno.h>
 #include <poll.h>
+#include <thread>
 #include <vector>
 #include <time.h>
 #include <atomic>
@@ -40,7 +41,7 @@ using namespace apelz4;
 struct APE_LZ4_rxbuf {
     char *data;
     size_t size, used;
-    int registered;
+    int registered;   // 1 registered for DMA, 0 not (yet), -1 never (a host-only buffer)
 };
 
 namespace {
@@ -49,8 +50,10 @@ inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
 inline int bound_of(int n) { return n + n / 255 + 16; }
 
 void rx_unregister(APE_LZ4_rxbuf *b) {
-    if (b->registered) (void)hipHostUnregister(b->data);
-    b->registered = 0;
+    if (b->registered == 1) {
+        (void)hipHostUnregister(b->data);
+        b->registered = 0;
+    }
 }
 
 int rx_register(APE_LZ4_rxbuf *b) {
@@ -186,7 +189,7 @@ int APE_LZ4_rxbuf_prepare(APE_LZ4_rxbuf *b, size_t more) {
 char *APE_LZ4_rxbuf_data(APE_LZ4_rxbuf *b) { return b ? b->data : nullptr; }
 size_t APE_LZ4_rxbuf_used(const APE_LZ4_rxbuf *b) { return b ? b->used : 0; }
 size_t APE_LZ4_rxbuf_room(const APE_LZ4_rxbuf *b) { return b ? b->size - b->used : 0; }
-int APE_LZ4_rxbuf_pinned(const APE_LZ4_rxbuf *b) { return b ? b->registered : 0; }
+int APE_LZ4_rxbuf_pinned(const APE_LZ4_rxbuf *b) { return b ? b->registered == 1 : 0; }
 
 // append raw bytes (what a read() into the buffer does); returns 0 or -1
 int APE_LZ4_rxbuf_append(APE_LZ4_rxbuf *b, const char *data, size_t len) {
@@ -259,12 +262,6 @@ void APE_LZ4_rxbuf_free(APE_LZ4_rxbuf *b) {
 // TX: compress nblocks blocks of block_size bytes (block i at h_src + i*src_stride) on the
 // current device, `batch` at a time, and write the framed stream to fd.  Returns the
 // bytes written, or a negative APE_LZ4_GPU_E* code.
-// The frame-pack kernel stores each batch's frames straight into a pinned, device-mapped
-// send buffer (zero-copy over PCIe), so no D2H copy waits for the batch's size: the host
-// only waits for the batch's kernels, then write()s the buffer while the GPU encodes and
-// packs the next ones into the other buffers.  kSlots batch slots: the
-// H2D of one batch, the kernels of another and the write() of a third overlap.
-constexpr int kSlots = 3;
 long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_stride,
                                      int block_size, int nblocks, int batch) {
     if (fd < 0 || !h_src || block_size <= 0 || block_size > kMaxBlock || nblocks < 0 || batch <= 0 ||
@@ -273,21 +270,22 @@ long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_strid
     int rc = APE_LZ4_gpu_init();
     if (rc) return rc;
     const size_t slot = up16((size_t)bound_of(block_size));
-    Dev d[kSlots];
-    char *hf[kSlots] = {}, *df[kSlots] = {};   // pinned send buffers: host / device views
-    long long *htot[kSlots] = {};
+    Dev d[2];
+    char *hf[2] = {nullptr, nullptr};
+    long long *htot[2] = {nullptr, nullptr};
     long long sent = 0;
+    int nb[2] = {0, 0};
     const int nbat = (nblocks + batch - 1) / batch;
-    for (int i = 0; i < kSlots && rc == 0; i++) {
+    for (int i = 0; i < 2 && rc == 0; i++) {
         if (dev_alloc(d[i], batch, block_size, true) != 0 ||
             hipHostMalloc((void **)&hf[i], (size_t)batch * (slot + 4) + 64, hipHostMallocDefault) != hipSuccess ||
-            hipHostGetDevicePointer((void **)&df[i], hf[i], 0) != hipSuccess ||
             hipHostMalloc((void **)&htot[i], sizeof(long long), hipHostMallocDefault) != hipSuccess)
             rc = APE_LZ4_GPU_ENOMEM;
     }
     auto launch = [&](int c) -> int {
-        Dev &D = d[c % kSlots];
+        Dev &D = d[c & 1];
         const int k = nblocks - c * batch < batch ? nblocks - c * batch : batch;
+        nb[c & 1] = k;
         const char *src = h_src + (size_t)c * batch * src_stride;
         (void)hipEventRecord(D.tev[0], D.st);
         hipError_t e = hipMemcpy2DAsync(D.src, (size_t)block_size, src, src_stride, (size_t)block_size,
@@ -297,40 +295,42 @@ long long APE_LZ4_socket_send_blocks(int fd, const char *h_src, size_t src_strid
         int r = APE_LZ4_compress_batch_strided_dev(D.src, (size_t)block_size, D.sizes, D.comp, slot,
                                                    nullptr, D.csz, k, D.st);
         if (r == 0) r = APE_LZ4_frame_offsets_dev(D.csz, D.off, D.scratch, k, D.st);
+        if (r == 0) r = APE_LZ4_frame_pack_strided_dev(D.comp, slot, D.csz, D.off, D.frames, k, D.st);
         if (r) return r;
         (void)hipEventRecord(D.tev[2], D.st);
-        r = APE_LZ4_frame_pack_strided_dev(D.comp, slot, D.csz, D.off, df[c % kSlots], k, D.st);
-        if (r) return r;
-        (void)hipEventRecord(D.tev[3], D.st);
-        e = hipMemcpyAsync(htot[c % kSlots], D.off + k, sizeof(long long), hipMemcpyDeviceToHost, D.st);
+        e = hipMemcpyAsync(htot[c & 1], D.off + k, sizeof(long long), hipMemcpyDeviceToHost, D.st);
         if (e == hipSuccess) e = hipEventRecord(D.ev, D.st);
         return e == hipSuccess ? 0 : APE_LZ4_GPU_ELAUNCH;
     };
     const long long ttx = now_ns();
-    for (int c = 0; c < kSlots - 1 && c < nbat && rc == 0; c++) rc = launch(c);
+    if (rc == 0 && nbat > 0) rc = launch(0);
     for (int c = 0; c < nbat && rc == 0; c++) {
-        Dev &D = d[c % kSlots];
+        Dev &D = d[c & 1];
         long long t0 = now_ns();
-        // the batch's kernels (frames already in hf) and its size
         if (hipEventSynchronize(D.ev) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
-        const long long tot = *htot[c % kSlots];
+        const long long tot = *htot[c & 1];
+        (void)hipEventRecord(D.tev[3], D.st);
+        if (hipMemcpyAsync(hf[c & 1], D.frames, (size_t)tot, hipMemcpyDeviceToHost, D.st) != hipSuccess ||
+            hipEventRecord(D.tev[4], D.st) != hipSuccess || hipStreamSynchronize(D.st) != hipSuccess) {
+            rc = APE_LZ4_GPU_ELAUNCH;
+            break;
+        }
         long long t1 = now_ns();
         sock_add(4, t1 - t0);
         sock_add(0, ev_ns(D.tev[0], D.tev[1]));
         sock_add(1, ev_ns(D.tev[1], D.tev[2]));
-        sock_add(2, ev_ns(D.tev[2], D.tev[3]));   // the pack: frames over PCIe into hf
+        sock_add(2, ev_ns(D.tev[3], D.tev[4]));
         sock_add(5, 1);
-        // batch c + kSlots - 1 into the slot batch c - 1 used (its write() is done)
-        if (c + kSlots - 1 < nbat) rc = launch(c + kSlots - 1);
+        if (c + 1 < nbat) rc = launch(c + 1);   // the next batch's GPU work under this write
         if (rc) break;
         t0 = now_ns();
-        const long long w = write_all(fd, hf[c % kSlots], (size_t)tot);
+        const long long w = write_all(fd, hf[c & 1], (size_t)tot);
         sock_add(3, now_ns() - t0);
         if (w < 0) { rc = APE_LZ4_GPU_EINVAL; break; }
         sent += w;
     }
     sock_add(6, now_ns() - ttx);
-    for (int i = 0; i < kSlots; i++) {
+    for (int i = 0; i < 2; i++) {
         dev_free(d[i]);
         if (hf[i]) (void)hipHostFree(hf[i]);
         if (htot[i]) (void)hipHostFree(htot[i]);
@@ -352,14 +352,13 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
     if (rc) return rc;
     const int maxc = bound_of(block_size);
     const size_t chunk = 4u << 20;   // read() granularity
-    Dev d[kSlots];
-    APE_LZ4_rxbuf *rb[kSlots];
-    long long *hoff[kSlots] = {};
-    bool busy[kSlots] = {};
-    long long base[kSlots] = {};  // first block of the batch in flight on d[i]
-    int cnt[kSlots] = {};         // ... and its block count
-    for (int i = 0; i < kSlots; i++) rb[i] = APE_LZ4_rxbuf_new(4u << 20);
-    for (int i = 0; i < kSlots && rc == 0; i++) {
+    Dev d[2];
+    APE_LZ4_rxbuf *rb[2] = {APE_LZ4_rxbuf_new(4u << 20), APE_LZ4_rxbuf_new(4u << 20)};
+    long long *hoff[2] = {nullptr, nullptr};
+    bool busy[2] = {false, false};
+    long long base[2] = {0, 0};   // first block of the batch in flight on d[i]
+    int cnt[2] = {0, 0};          // ... and its block count
+    for (int i = 0; i < 2 && rc == 0; i++) {
         if (!rb[i] || dev_alloc(d[i], batch, block_size, false) != 0 ||
             hipHostMalloc((void **)&hoff[i], ((size_t)batch + 1) * sizeof(long long),
                           hipHostMallocDefault) != hipSuccess)
@@ -395,9 +394,8 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
             b->used += (size_t)r;
             continue;
         }
-        // a full batch: hand this buffer to the GPU, continue receiving in the next one (free
-        // once the batch kSlots - 1 back has finished: kSlots - 1 batches stay in flight)
-        const int nxt = (cur + 1) % kSlots;
+        // a full batch: hand this buffer to the GPU, continue receiving in the other one
+        const int nxt = cur ^ 1;
         if (busy[nxt]) {
             t0 = now_ns();
             if (hipStreamSynchronize(d[nxt].st) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
@@ -443,7 +441,7 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
         parsed = 0;
     }
     sock_add(7, now_ns() - trx);
-    for (int i = 0; i < kSlots; i++) {   // drain every batch in flight, whatever rc is
+    for (int i = 0; i < 2; i++) {   // drain every batch in flight, whatever rc is
         if (!busy[i]) continue;
         if (hipStreamSynchronize(d[i].st) != hipSuccess) {
             if (rc == 0) rc = APE_LZ4_GPU_ELAUNCH;   // its results never reached h_result
@@ -457,7 +455,7 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
             memcpy(h_result + base[i], d[i].hres, (size_t)cnt[i] * sizeof(int));
         }
     }
-    for (int i = 0; i < kSlots; i++) {
+    for (int i = 0; i < 2; i++) {
         dev_free(d[i]);
         APE_LZ4_rxbuf_free(rb[i]);
         if (hoff[i]) (void)hipHostFree(hoff[i]);
@@ -533,7 +531,9 @@ __global__ void chain_rx_setup(const char *stage, const long long *poff, char *w
 
 }  // namespace
 
-struct APE_LZ4_chain {
+// One part of a chain: a subset of the connections served by one host thread with its own
+// streams and buffers (APE_LZ4_chain below splits the connections over kChainThreads parts).
+struct ChainPart {
     int dev = 0, nconn = 0, msg = 0, nch = 0, K = 1, nt = 0;   // nt = chunks of a full round
     size_t W = 0;
     // TX (one thread): device window, compressed slots, frames, pointer arrays
@@ -565,7 +565,7 @@ struct APE_LZ4_chain {
 
 namespace {
 
-void chain_release(APE_LZ4_chain *c) {
+void chain_release(ChainPart *c) {
     if (c->tst) (void)hipStreamSynchronize(c->tst);
     if (c->rst) (void)hipStreamSynchronize(c->rst);
     for (void *p : {(void *)c->txwin, (void *)c->slots, (void *)c->csz,
@@ -609,14 +609,9 @@ hipError_t chain_slide(char *win, size_t W, int nconn, uint32_t &pos, size_t nee
 
 inline int chunk_len(int msg, int j) { return msg - kChunk * j < kChunk ? msg - kChunk * j : kChunk; }
 
-}  // namespace
-
-extern "C" {
-
-APE_LZ4_chain *APE_LZ4_chain_new(int nconn, int msg_len) {
-    if (nconn <= 0 || msg_len <= 0 || msg_len > (1 << 24) || APE_LZ4_gpu_init() != 0) return nullptr;
-    APE_LZ4_chain *c = new APE_LZ4_chain();
-    (void)hipGetDevice(&c->dev);
+ChainPart *part_new(int nconn, int msg_len, int dev) {
+    ChainPart *c = new ChainPart();
+    c->dev = dev;
     c->nconn = nconn;
     c->msg = msg_len;
     c->nch = (msg_len + kChunk - 1) / kChunk;
@@ -652,16 +647,11 @@ APE_LZ4_chain *APE_LZ4_chain_new(int nconn, int msg_len) {
     return c;
 }
 
-void APE_LZ4_chain_free(APE_LZ4_chain *c) {
-    if (c) chain_release(c);
-}
-
-// TX: nmsg messages per connection (message m of connection i at h_msgs + (m * nconn + i) *
-// msg_stride) as the reference's frames on fds[i], in rounds of K messages.  Returns the bytes
-// written or an error code.
-long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msgs,
-                             size_t msg_stride, int nmsg) {
-    if (!c || !fds || !h_msgs || nmsg < 0 || msg_stride < (size_t)c->msg) return APE_LZ4_GPU_EINVAL;
+// TX of one part: nmsg messages per connection (message m of local connection i at h_msgs +
+// m * row_pitch + i * msg_stride) as the reference's frames on fds[i], in rounds of K messages.
+// Returns the bytes written or an error code.
+long long part_send(ChainPart *c, const int *fds, const char *h_msgs, size_t msg_stride,
+                    size_t row_pitch, int nmsg) {
     if (hipSetDevice(c->dev) != hipSuccess) return APE_LZ4_GPU_ENODEV;
     const int M = c->nconn, nch = c->nch, nr = (nmsg + c->K - 1) / c->K;
     long long sent = 0;
@@ -672,7 +662,7 @@ long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msg
         if (chain_slide(c->txwin, c->W, M, c->txpos, (size_t)k * c->msg, c->tst) != hipSuccess)
             return APE_LZ4_GPU_ELAUNCH;
         for (int mm = 0; mm < k; mm++) {
-            const char *h = h_msgs + (size_t)(r * c->K + mm) * M * msg_stride;
+            const char *h = h_msgs + (size_t)(r * c->K + mm) * row_pitch;
             if (hipMemcpy2DAsync(c->txwin + c->txpos + (size_t)mm * c->msg, c->W, h, msg_stride,
                                  (size_t)c->msg, (size_t)M, hipMemcpyHostToDevice, c->tst) != hipSuccess)
                 return APE_LZ4_GPU_ELAUNCH;
@@ -722,15 +712,13 @@ long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msg
     return rc ? rc : sent;
 }
 
-// RX: nmsg messages per connection, in rounds of K; message m of connection i is decoded into
-// h_out + (m * nconn + i) * out_stride.  h_status[i] = 0, or the first failing chunk's result
-// (decompress_safe_continue's value, or the wrong size it produced); a failing connection
-// makes the call return APE_LZ4_GPU_EINVAL.  Returns the payload bytes delivered or an error
-// code (EINVAL also for a malformed frame or an early EOF).
-long long APE_LZ4_chain_recv(APE_LZ4_chain *c, const int *fds, char *h_out, size_t out_stride,
-                             int nmsg, int *h_status) {
-    if (!c || !fds || !h_out || !h_status || nmsg < 0 || out_stride < (size_t)c->msg)
-        return APE_LZ4_GPU_EINVAL;
+// RX of one part: nmsg messages per connection, in rounds of K; message m of local connection i
+// is decoded into h_out + m * row_pitch + i * out_stride.  h_status[i] = 0, or the first failing
+// chunk's result (decompress_safe_continue's value, or the wrong size it produced); a failing
+// connection makes the call return APE_LZ4_GPU_EINVAL.  Returns the payload bytes delivered or
+// an error code (EINVAL also for a malformed frame or an early EOF).
+long long part_recv(ChainPart *c, const int *fds, char *h_out, size_t out_stride, size_t row_pitch,
+                    int nmsg, int *h_status) {
     if (hipSetDevice(c->dev) != hipSuccess) return APE_LZ4_GPU_ENODEV;
     const int M = c->nconn, nch = c->nch, nr = (nmsg + c->K - 1) / c->K;
     const int maxf = c->K * nch;   // frames of a full round per connection
@@ -741,10 +729,11 @@ long long APE_LZ4_chain_recv(APE_LZ4_chain *c, const int *fds, char *h_out, size
     std::vector<pollfd> pf((size_t)M);
     std::vector<int> pmap((size_t)M);
     int rc = 0;
-    for (int i = 0; i < M; i++) {
-        h_status[i] = 0;
-        rb[i] = APE_LZ4_rxbuf_new(1u << 16);
-        if (!rb[i]) rc = APE_LZ4_GPU_ENOMEM;
+    for (int i = 0; i < M; i++) {   // host-only buffers: the payloads go to the GPU through
+        h_status[i] = 0;            // the pinned staging area, so no per-connection registration
+        rb[i] = (APE_LZ4_rxbuf *)calloc(1, sizeof(APE_LZ4_rxbuf));
+        if (rb[i]) rb[i]->registered = -1;
+        if (!rb[i] || APE_LZ4_rxbuf_prepare(rb[i], 1u << 16) != 0) rc = APE_LZ4_GPU_ENOMEM;
     }
     auto round_k = [&](int r) { return nmsg - r * c->K < c->K ? nmsg - r * c->K : c->K; };
     long long got = 0;
@@ -861,7 +850,7 @@ long long APE_LZ4_chain_recv(APE_LZ4_chain *c, const int *fds, char *h_out, size
         }
         if (rc) break;
         for (int mm = 0; mm < k && e == hipSuccess; mm++)
-            e = hipMemcpy2DAsync(h_out + (size_t)(r * c->K + mm) * M * out_stride, out_stride,
+            e = hipMemcpy2DAsync(h_out + (size_t)(r * c->K + mm) * row_pitch, out_stride,
                                  c->rxwin + c->rxpos + (size_t)mm * c->msg, c->W, (size_t)c->msg,
                                  (size_t)M, hipMemcpyDeviceToHost, c->rst);
         if (e == hipSuccess)
@@ -888,6 +877,95 @@ long long APE_LZ4_chain_recv(APE_LZ4_chain *c, const int *fds, char *h_out, size
     sock_add(7, now_ns() - t_all);
     for (int i = 0; i < M; i++) APE_LZ4_rxbuf_free(rb[i]);
     return rc ? rc : got;
+}
+
+// parts per chain: each part's socket I/O, staging and launches run on a host thread of its
+// own (the syscalls of many small frames are what one thread cannot keep up with)
+constexpr int kChainThreads = 8;
+
+}  // namespace
+
+struct APE_LZ4_chain {
+    int nconn = 0, msg = 0, nparts = 0;
+    int first[kChainThreads + 1] = {};
+    ChainPart *part[kChainThreads] = {};
+};
+
+namespace {
+
+// run f(p) for every part, parts 1.. on threads of their own, part 0 on the caller's; the
+// first error (in part order) or the sum of the results
+template <typename F>
+long long chain_parallel(APE_LZ4_chain *c, F f) {
+    long long res[kChainThreads] = {};
+    std::vector<std::thread> th;
+    for (int p = 1; p < c->nparts; p++) th.emplace_back([&, p] { res[p] = f(p); });
+    res[0] = f(0);
+    for (auto &t : th) t.join();
+    long long sum = 0;
+    for (int p = 0; p < c->nparts; p++) {
+        if (res[p] < 0) return res[p];
+        sum += res[p];
+    }
+    return sum;
+}
+
+}  // namespace
+
+extern "C" {
+
+APE_LZ4_chain *APE_LZ4_chain_new(int nconn, int msg_len) {
+    if (nconn <= 0 || msg_len <= 0 || msg_len > (1 << 24) || APE_LZ4_gpu_init() != 0) return nullptr;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    APE_LZ4_chain *c = new APE_LZ4_chain();
+    c->nconn = nconn;
+    c->msg = msg_len;
+    int np = 4;
+    if (const char *ev = getenv("APE_LZ4_CHAIN_THREADS")) np = atoi(ev);
+    np = np < 1 ? 1 : (np > kChainThreads ? kChainThreads : np);
+    c->nparts = np < nconn ? np : nconn;
+    for (int p = 0; p <= c->nparts; p++) c->first[p] = (int)((long long)p * nconn / c->nparts);
+    for (int p = 0; p < c->nparts; p++) {
+        c->part[p] = part_new(c->first[p + 1] - c->first[p], msg_len, dev);
+        if (!c->part[p]) {
+            APE_LZ4_chain_free(c);
+            return nullptr;
+        }
+    }
+    return c;
+}
+
+void APE_LZ4_chain_free(APE_LZ4_chain *c) {
+    if (!c) return;
+    for (int p = 0; p < c->nparts; p++)
+        if (c->part[p]) chain_release(c->part[p]);
+    delete c;
+}
+
+// TX: nmsg messages per connection (message m of connection i at h_msgs + (m * nconn + i) *
+// msg_stride) as the reference's frames on fds[i].  Returns the bytes written or an error code.
+long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msgs,
+                             size_t msg_stride, int nmsg) {
+    if (!c || !fds || !h_msgs || nmsg < 0 || msg_stride < (size_t)c->msg) return APE_LZ4_GPU_EINVAL;
+    return chain_parallel(c, [&](int p) {
+        const int i0 = c->first[p];
+        return part_send(c->part[p], fds + i0, h_msgs + (size_t)i0 * msg_stride, msg_stride,
+                         (size_t)c->nconn * msg_stride, nmsg);
+    });
+}
+
+// RX: nmsg messages per connection; message m of connection i is decoded into h_out + (m *
+// nconn + i) * out_stride; h_status[i] as part_recv.  Returns the payload bytes or an error code.
+long long APE_LZ4_chain_recv(APE_LZ4_chain *c, const int *fds, char *h_out, size_t out_stride,
+                             int nmsg, int *h_status) {
+    if (!c || !fds || !h_out || !h_status || nmsg < 0 || out_stride < (size_t)c->msg)
+        return APE_LZ4_GPU_EINVAL;
+    return chain_parallel(c, [&](int p) {
+        const int i0 = c->first[p];
+        return part_recv(c->part[p], fds + i0, h_out + (size_t)i0 * out_stride, out_stride,
+                         (size_t)c->nconn * out_stride, nmsg, h_status + i0);
+    });
 }
 
 }  // extern "C"

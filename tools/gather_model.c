@@ -45,6 +45,8 @@ static int lines(uint32_t *a, int n) {   /* distinct 128-B lines among byte rang
 int main(int argc, char **argv)
 {
     const int n = 65536, nb = argc > 1 ? atoi(argv[1]) : 16, lag = 3;
+    const int pol = argc > 2 ? atoi(argv[2]) : 7;   /* 7: the product; 8: T whenever it verifies, else L;
+                                                       9: L whenever it verifies, else T */
     uint8_t *buf = malloc((size_t)n * nb + 16);
     synth_blocks(buf, n, n, 0, nb, 1);
     long steps = 0, l_all = 0, l_valid = 0, l_ver = 0, l_tag = 0, lanes = 0, valid = 0, ver = 0,
@@ -101,7 +103,14 @@ int main(int argc, char **argv)
                         if (ok[j]) { l[j] = 4; while (p + l[j] < mlimit && in[p + l[j]] == in[c + l[j]]) l[j]++; }
                     }
                     int pick = -1, l12 = l[1] < 12 ? l[1] : 12;
-                    if (ok[1] && (!ok[0] || (l[0] < 12 && l12 >= l[0]))) pick = 1;
+                    if (pol == 8) pick = ok[0] ? 0 : (ok[1] ? 1 : -1);
+                    else if (pol == 9) pick = ok[1] ? 1 : (ok[0] ? 0 : -1);
+                    else if (pol == 10) {   /* L measured to 8 bytes only */
+                        int l8 = l[1] < 8 ? l[1] : 8;
+                        if (ok[1] && (!ok[0] || (l[0] < 8 && l8 >= l[0]))) pick = 1;
+                        else if (ok[0]) pick = 0;
+                    }
+                    else if (ok[1] && (!ok[0] || (l[0] < 12 && l12 >= l[0]))) pick = 1;
                     else if (ok[0]) pick = 0;
                     if (pick >= 0) { best = l[pick]; bc = cs[pick]; usedT = pick == 0; }
                 }
