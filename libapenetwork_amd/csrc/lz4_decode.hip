@@ -61,6 +61,9 @@ constexpr int kWinNeed = 84;     // a parse window reads up to P + 63 + 21
 constexpr int kBatch = 64;       // descriptors per copy batch (one per lane)
 constexpr int kMaxDesc = kBatch + 44;   // held before a copy: <= 63, + <= 44 per parse step, + 1
 constexpr uint32_t kLaneMax = 64;  // longest match one lane copies (4 x 16 bytes)
+#ifndef APE_LZ4_DUNITS
+#define APE_LZ4_DUNITS 1           // lane matches load / store only the 16-byte units they need
+#endif
 
 struct __attribute__((aligned(16))) WaveLds {
     uint8_t win[kWinB + 64];     // output [base, base + kWinB) (+ slack for 16-byte reads)
@@ -522,6 +525,45 @@ __device__ __forceinline__ void lane_match(WaveLds &L, const Dec &D, uint32_t ba
     uint8_t *w = L.win + (ma - base);
     const int ps = (int)ma - (int)off;
     const bool big = n >= 16u;
+#if APE_LZ4_DUNITS
+    // Only the units a lane needs: unit k (k = 1..3) exists when n > 16 k.  Lanes whose
+    // match is shorter issue no load for it, so a gather instruction touches only the lines
+    // its active lanes need (the texture path's cost is per line: tools/ubench/gather_rate).
+    // The placeholders start at 0, not at v0, so no unit waits for another's load.
+    const uint32_t t1 = umin(16u, n - 16u), t2 = umin(32u, n - 16u), t3 = n - 16u;
+    const bool u1 = n > 16u, u2 = n > 32u, u3 = n > 48u;
+    uint4 v0, v1 = make_uint4(0, 0, 0, 0), v2 = v1, v3 = v1;
+    if (off != 0u && off < n) {   // overlaps itself (off >= 16, n > 16): unit after unit
+        const uint8_t *s = L.win + ((uint32_t)ps - base);
+        lds_st16(w, lds16(s));
+        if (u1) lds_st16(w + t1, lds16(s + t1));
+        if (u2) lds_st16(w + t2, lds16(s + t2));
+        if (u3) lds_st16(w + t3, lds16(s + t3));
+        return;
+    }
+    if (!glb) {   // (offset 0: in-window bytes, zeroed below)
+        const uint8_t *s = L.win + ((uint32_t)ps - base);
+        v0 = lds16(s);
+        if (u1) v1 = lds16(s + t1);
+        if (u2) v2 = lds16(s + t2);
+        if (u3) v3 = lds16(s + t3);
+    } else {
+        gcu8 *s = (DICT && ps < 0) ? D.dend + ps : (gcu8 *)D.dst + ps;
+        v0 = gload16_nt(s);
+        if (u1) v1 = gload16_nt(s + t1);
+        if (u2) v2 = gload16_nt(s + t2);
+        if (u3) v3 = gload16_nt(s + t3);
+    }
+    if (off == 0u) v0 = v1 = v2 = v3 = make_uint4(0, 0, 0, 0);
+    if (big) {
+        lds_st16(w, v0);
+        if (u1) lds_st16(w + t1, v1);
+        if (u2) lds_st16(w + t2, v2);
+        if (u3) lds_st16(w + t3, v3);
+    } else {
+        lds_put_small<true>(w, v0, n);
+    }
+#else
     // unit offsets: 0, 16, 32, 48 clamped to n - 16 (repeats rewrite the same bytes)
     const uint32_t t1 = big ? umin(16u, n - 16u) : 0u, t2 = big ? umin(32u, n - 16u) : 0u,
                    t3 = big ? umin(48u, n - 16u) : 0u;
@@ -559,6 +601,7 @@ __device__ __forceinline__ void lane_match(WaveLds &L, const Dec &D, uint32_t ba
     } else {
         lds_put_small<true>(w, v0, n);
     }
+#endif
 }
 
 // Per-lane sequence of the batch: literal [o, m) from input ls, match [m, me) at offset off.
