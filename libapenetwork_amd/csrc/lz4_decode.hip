@@ -11,8 +11,8 @@
 //         64 candidate token positions P..P+63 every lane speculatively parses
 //         "the sequence that would start at P+lane" (token, literal length,
 //         offset, one match-length extension byte) and its successor position.
-//         The scalar unit then follows the true chain from P through those
-//         successors (one v_readlane per sequence); a wave prefix-sum gives each
+//         The true chain from P through those successors is found by binary
+//         lifting (ds_bpermute rounds, no serial walk); a wave prefix-sum gives each
 //         member its output position, and every member applies the reference's
 //         checks (:1345-1444) in the reference's order, so the first failing
 //         sequence returns the identical -(ip)-1.  Rare "complex" tokens

@@ -1386,6 +1386,14 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
     E.bigm = 0;
     E.r = E.lit = E.mlm4 = E.off = E.ba = 0;
     __syncthreads();
+#ifdef APE_EXP_NOEMIT   // diagnostic: instruction count without the emitter (no output)
+    for (int s = k0; s < nsteps; s++) {
+        __syncthreads();
+        __syncthreads();
+    }
+    if (lane == 0) *result = 0;
+    return;
+#endif
     for (int s = k0; s < nsteps; s++) {
         // S.qn: the walker's count as of its last publish (before the previous barrier)
         const uint32_t avail = (uint32_t)__builtin_amdgcn_readfirstlane(S.qn) - E.qc;
