@@ -5,8 +5,8 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 for v in "$@"; do
   lib=$PWD/libapenetwork_amd/libape_lz4_amd_$v.so
   [ "$v" = base ] && lib=$PWD/libapenetwork_amd/libape_lz4_amd.so
-  rm -rf gpurun_out/sq
-  APE_LZ4_LIB=$lib timeout -k 10 300 bash tools/sq_passes.sh ${NB:-16384} > gpurun_out/sqv_$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/sqv_$v.log; exit 1; }
+  rm -rf gpurun_out/sqv_$v
+  SQ_DIR=gpurun_out/sqv_$v APE_LZ4_LIB=$lib timeout -k 10 300 bash tools/sq_passes.sh ${NB:-16384} > gpurun_out/sqv_$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/sqv_$v.log; exit 1; }
   python3 - $v ${NB:-16384} <<'PY'
 import sys, re, ast
 v, nb = sys.argv[1], int(sys.argv[2])
