@@ -21,8 +21,9 @@ oracle = the reference decoder restated) and the compression ratio is reported.
 
 Also in the line (rank 0, N = 1): `config2` = BASELINE config 2 (256K x 4 KiB random blocks
 compressed by the reference algorithm, decode only) with its own roofline and CPU baseline;
-`config5` = BASELINE config 5 through a real byte path: GPU encode -> frames -> one loopback
-TCP connection -> pinned growable rxbuf + frame parser -> GPU decode (sock_leg, 1 GiB);
+`config5` = BASELINE config 5 through a real byte path: GPU encode -> frames -> loopback TCP
+connection(s) (--sock-conns, default 1) -> pinned growable rxbuf + frame
+parser -> GPU decode (sock_leg, 8 GiB);
 `cpu_baseline` = the reference src/ape_lz4.c built from its own source with gcc and clang
 (oracle/_ref), a 1..N thread sweep over the box's usable cores on a 4 GiB sample;
 `roofline` = the dominant kernel's algorithmic bytes / its HIP-event time, plus the
@@ -531,14 +532,16 @@ def stream_bench(args):
 
 
 def sock_leg(args):
-    """BASELINE config 5 through a real byte path: a loopback TCP connection.
+    """BASELINE config 5 through a real byte path: loopback TCP connections.
 
-    TX thread: APE_LZ4_socket_send_blocks -- host blocks --H2D--> encode --> frames
-    --D2H--> write().  RX (this thread): APE_LZ4_socket_recv_blocks -- read() into the
+    Per connection, a TX thread: APE_LZ4_socket_send_blocks -- host blocks --H2D--> encode
+    --> frames --D2H--> write(); an RX thread: APE_LZ4_socket_recv_blocks -- read() into the
     pinned growable rxbuf (the ape_buffer analogue) --> frame parser (K7 rewritten) --H2D-->
     decode from the frames --D2H--> host blocks.  Both sides double-buffer, so the socket
-    I/O of one batch overlaps the GPU work of the next.  Rate = uncompressed bytes / wall
-    time from the first send to the last received block; every block is compared."""
+    I/O of one batch overlaps the GPU work of the next.  The blocks are split contiguously
+    over --sock-conns connections (a server's sockets share one GPU); the one-connection run
+    is reported beside it.  Rate = uncompressed bytes / wall time from the first send to the
+    last received block; every block is compared."""
     import socket
     import threading
 
@@ -563,87 +566,133 @@ def sock_leg(args):
     del g
     src_np, dst_np = h_src.numpy(), h_dst.numpy()
 
-    def run(k):
-        srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
-        srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-        srv.bind(("127.0.0.1", 0))
-        srv.listen(1)
-        tx = socket.create_connection(srv.getsockname())
-        rx, _ = srv.accept()
-        srv.close()
-        for s_ in (tx, rx):
-            s_.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
-            s_.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
-        sent = {}
+    def run(k, conns):
+        """k blocks over `conns` connections (contiguous shares), a TX and an RX thread each."""
+        pairs = []
+        for _ in range(conns):
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind(("127.0.0.1", 0))
+            srv.listen(1)
+            tx = socket.create_connection(srv.getsockname())
+            rx, _ = srv.accept()
+            srv.close()
+            for s_ in (tx, rx):
+                s_.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
+                s_.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
+            pairs.append((tx, rx))
+        cut = [k * c // conns for c in range(conns + 1)]
+        out = [{} for _ in range(conns)]
 
-        def txf():
+        def txf(c):
+            tx, lo, hi = pairs[c][0], cut[c], cut[c + 1]
             try:
-                sent["bytes"] = amd.socket_send_blocks(tx.fileno(), src_np[:k], n, batch)
+                out[c]["sent"] = amd.socket_send_blocks(tx.fileno(), src_np[lo:hi], n, batch)
             except Exception as e:   # reported below
-                sent["err"] = e
+                out[c]["err"] = e
             finally:
                 tx.shutdown(socket.SHUT_WR)
 
-        t0 = time.perf_counter()
-        th = threading.Thread(target=txf)
-        th.start()
-        got = amd.socket_recv_blocks(rx.fileno(), dst_np[:k], n, batch, res[:k])
-        th.join()
-        wall = time.perf_counter() - t0
-        tx.close()
-        rx.close()
-        if "err" in sent:
-            raise sent["err"]
-        return wall, got, sent["bytes"]
+        def rxf(c):
+            rx, lo, hi = pairs[c][1], cut[c], cut[c + 1]
+            try:
+                out[c]["got"] = amd.socket_recv_blocks(rx.fileno(), dst_np[lo:hi], n, batch,
+                                                       res[lo:hi])
+            except Exception as e:
+                out[c]["err"] = e
 
-    run(min(nb, 2 * batch))                    # warm-up (kernels, allocations)
-    h_dst.zero_()
-    amd.socket_stats(reset=True)
-    wall, got, wire = run(nb)
-    split = amd.socket_stats(reset=True)
-    ok = got == nb and bool((res == n).all()) and bool(torch.equal(h_dst, h_src))
-    # the same wire bytes through the same kind of connection without the codec
-    ceiling, ceiling_cold = sock_ceilings(int(wire))
+        ths = [threading.Thread(target=f, args=(c,)) for c in range(conns) for f in (txf, rxf)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        wall = time.perf_counter() - t0
+        for tx, rx in pairs:
+            tx.close()
+            rx.close()
+        for o in out:
+            if "err" in o:
+                raise o["err"]
+        return wall, sum(o["got"] for o in out), sum(o["sent"] for o in out)
+
+    def measure(conns):
+        h_dst.zero_()
+        res[:] = -9
+        amd.socket_stats(reset=True)
+        wall, got, wire = run(nb, conns)
+        split = amd.socket_stats(reset=True)
+        ok = got == nb and bool((res == n).all()) and bool(torch.equal(h_dst, h_src))
+        # the same wire bytes through as many connections without the codec
+        ceiling, ceiling_cold = sock_ceilings(int(wire), conns)
+        r = {"value": round(nb * n / wall / GIB, 3), "connections": conns,
+             "wall_s": round(wall, 3), "wire_bytes": int(wire),
+             "ratio": round(nb * n / (wire - 4 * nb), 4),
+             "wire_GBps": round(wire / wall / 1e9, 3), "verified": ok,
+             "ceiling_GBps": ceiling, "ceiling_cold_GBps": ceiling_cold,
+             "wire_frac_of_ceiling": round(wire / wall / 1e9 / ceiling, 3) if ceiling else None,
+             "wire_frac_of_cold_ceiling": (round(wire / wall / 1e9 / ceiling_cold, 3)
+                                           if ceiling_cold else None),
+             "split_ms": split}
+        r["bound"] = ("socket" if ceiling_cold and r["wire_GBps"] >= 0.8 * ceiling_cold
+                      else "pipeline")
+        return r
+
+    conns = max(1, args.sock_conns)
+    run(min(nb, 2 * batch * conns), conns)      # warm-up (kernels, allocations)
+    main = measure(conns)
+    one = measure(1) if conns > 1 else None
     cpu = None if args.no_cpu_baseline else cpu_sock_baseline(n)
     line = {
-        "metric": "LZ4 GiB/s through a loopback TCP socket (GPU encode -> frames -> socket -> "
+        "metric": "LZ4 GiB/s through loopback TCP sockets (GPU encode -> frames -> socket -> "
                   "pinned rxbuf -> GPU decode), BASELINE config 5",
-        "value": round(nb * n / wall / GIB, 3), "unit": "GiB/s", "n_gpus": 1,
+        "value": main["value"], "unit": "GiB/s", "n_gpus": 1,
         "higher_is_better": True, "dtype": "u8",
         "data": "synthetic (SURVEY App. C gen_%s)" % args.kind,
-        "config": {"workload": "%d x %d KiB blocks over one 127.0.0.1 TCP connection, %d blocks "
-                               "per GPU batch" % (nb, n >> 10, batch)},
-        "wall_s": round(wall, 3), "wire_bytes": int(wire), "ratio": round(nb * n / (wire - 4 * nb), 4),
-        "wire_GBps": round(wire / wall / 1e9, 3), "verified": ok,
-        "ceiling_GBps": ceiling, "ceiling_cold_GBps": ceiling_cold,
-        "wire_frac_of_ceiling": round(wire / wall / 1e9 / ceiling, 3) if ceiling else None,
-        "wire_frac_of_cold_ceiling": round(wire / wall / 1e9 / ceiling_cold, 3) if ceiling_cold else None,
-        "ceiling": "plain bytes over one 127.0.0.1 TCP connection, 4 MiB write()s / read()s, no "
-                   "codec, same wire bytes (oracle/cpu_bench.c sock_ceiling_buf): ceiling_GBps "
-                   "with one 4 MiB buffer per side (cache-hot), ceiling_cold_GBps walking 1 GiB "
-                   "buffers (every syscall copies cache-cold memory, as the codec path's do: its "
-                   "frames arrive by DMA and its receive buffer is read by DMA)",
-        "split_ms": split,
-        "split_note": "GPU phases from timing events per batch (they overlap each other and "
-                      "the socket I/O: double-buffered); write/read = time in the syscalls; "
-                      "gpu_wait = host blocked on the GPU",
+        "config": {"workload": "%d x %d KiB blocks over %d 127.0.0.1 TCP connection(s) (a TX and "
+                               "an RX thread each, contiguous shares), %d blocks per GPU batch" % (
+                                   nb, n >> 10, conns, batch)},
+        **{k: v for k, v in main.items() if k != "value"},
+        "ceiling": "plain bytes over as many 127.0.0.1 TCP connections in parallel, 4 MiB "
+                   "write()s / read()s, no codec, same wire bytes (oracle/cpu_bench.c "
+                   "sock_ceiling_buf): ceiling_GBps with one 4 MiB buffer per side (cache-hot), "
+                   "ceiling_cold_GBps walking 1 GiB buffers (every syscall copies cache-cold "
+                   "memory, as the codec path's do: its frames arrive by DMA and its receive "
+                   "buffer is read by DMA)",
+        "split_note": "summed over the connections; GPU phases from timing events per batch (they "
+                      "overlap each other and the socket I/O: double-buffered); write/read = time "
+                      "in the syscalls; gpu_wait = host blocked on the GPU",
+        "one_connection": one,
         "cpu_baseline": cpu,
     }
-    line["bound"] = ("socket" if ceiling_cold and line["wire_GBps"] >= 0.8 * ceiling_cold
-                     else "pipeline")
     return line
 
 
-def sock_ceilings(nbytes):
-    """(hot, cold) plain-bytes loopback rates in GB/s for nbytes (oracle/cpu_bench.c)."""
+def sock_ceilings(nbytes, conns=1):
+    """(hot, cold) plain-bytes loopback rates in GB/s for nbytes over `conns` connections in
+    parallel (oracle/cpu_bench.c; one thread pair per connection, ctypes releases the GIL):
+    total bytes / the slowest connection's time."""
+    import threading
     try:
         cb = C.CDLL(os.path.join(ROOT, "oracle", "libcpubench.so"))
         cb.sock_ceiling_buf.argtypes = [C.c_longlong, C.c_int, C.c_longlong, C.POINTER(C.c_double)]
-        o2 = (C.c_double * 2)()
         res = []
         for buf in (4 << 20, 1 << 30):
-            res.append(round(o2[1] / o2[0] / 1e9, 3)
-                       if cb.sock_ceiling_buf(nbytes, 4 << 20, buf, o2) == 0 else None)
+            outs = [(C.c_double * 2)() for _ in range(conns)]
+            rcs = [None] * conns
+            per = max(4 << 20, nbytes // conns)
+
+            def one(c):
+                rcs[c] = cb.sock_ceiling_buf(per, 4 << 20, buf, outs[c])
+
+            ths = [threading.Thread(target=one, args=(c,)) for c in range(conns)]
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+            ok = all(r == 0 for r in rcs)
+            res.append(round(sum(o[1] for o in outs) / max(o[0] for o in outs) / 1e9, 3)
+                       if ok else None)
         return tuple(res)
     except OSError:
         return None, None
@@ -986,6 +1035,8 @@ def main():
     ap.add_argument("--sock-blocks", type=int, default=1 << 17,
                     help="config 5 sample (131072 x 64 KiB = 8 GiB)")
     ap.add_argument("--sock-batch", type=int, default=2048)
+    ap.add_argument("--sock-conns", type=int, default=1,
+                    help="config 5: loopback connections in parallel (a TX and an RX thread each)")
     ap.add_argument("--sock-chained", action="store_true",
                     help="the reference wire format (chained 8 KiB blocks) over many sockets")
     ap.add_argument("--chain-conns", type=int, default=512)
