@@ -136,6 +136,9 @@ static_assert(kFetchAt < kEmitAll, "a fetch precedes emit_all");
 #ifndef APE_LZ4_ACC_L
 #define APE_LZ4_ACC_L 1
 #endif
+#ifndef APE_LZ4_CAPBITS
+#define APE_LZ4_CAPBITS 1            // length caps folded into the bit-index mins (v_min3)
+#endif
 #ifndef APE_EMIT_EVERY
 #define APE_EMIT_EVERY 8             // emitter: a batch every this many steps (at most)
 #endif
@@ -320,9 +323,14 @@ __device__ __forceinline__ uint32_t first_diff_bit(const uint32_t (&A)[NA], cons
     return m;
 }
 
-// common length of X and Y from byte 4 (dword 1) on, up to kEagerLen
+// common length of X and Y from byte 4 (dword 1) on, up to kEagerLen.  The cap is applied to
+// the bit index (one v_min3 with the dwords' own min) instead of to the byte count afterwards
 __device__ __forceinline__ uint32_t eager(const uint32_t (&X)[6], const uint32_t (&Y)[6]) {
+#if APE_LZ4_CAPBITS
+    return (umin(first_diff_bit<2, kYW>(X, Y), 8u * (kEagerLen - 4u)) >> 3) + 4u;
+#else
     return umin((first_diff_bit<2, kYW>(X, Y) >> 3) + 4u, kEagerLen);
+#endif
 }
 
 // bytes equal just before the match (in[p-1] == in[c-1], ...), 0..4
@@ -579,14 +587,23 @@ __device__ __forceinline__ uint32_t stage2_len(const EncLds &S, int lane, uint32
                                                const uint32_t (&E)[4]) {
     const uint4 o = ring16(S, eo);
     const uint32_t O[4] = {o.x, o.y, o.z, o.w};
-    uint32_t d = __builtin_elementwise_add_sat(first_diff_bit<0, 4>(O, E),
-                                               128u * ((uint32_t)lane & 3u));
+    const uint32_t li = 128u * ((uint32_t)lane & 3u);
+#if APE_LZ4_CAPBITS   // the cap 8 kExt2 bits joins the lane's own min (no min after the quad's)
+    uint32_t d = umin(first_diff_bit<0, 4>(O, E), 8u * kExt2 - li) + li;   // (no overflow)
+#else
+    uint32_t d = __builtin_elementwise_add_sat(first_diff_bit<0, 4>(O, E), li);
+#endif
     d = umin(d, dpp<0xB1>(0u, d));   // quad_perm [1,0,3,2]
     d = umin(d, dpp<0x4E>(0u, d));   // quad_perm [2,3,0,1]
-#if APE_LZ4_S2RUN   // continuation point + length: a run member subtracts its own
-    return eo + umin(d >> 3, kExt2);
+#if APE_LZ4_CAPBITS
+    const uint32_t len = d >> 3;     // <= kExt2
 #else
-    return umin(d >> 3, kExt2);
+    const uint32_t len = umin(d >> 3, kExt2);
+#endif
+#if APE_LZ4_S2RUN   // continuation point + length: a run member subtracts its own
+    return eo + len;
+#else
+    return len;
 #endif
 }
 
@@ -633,7 +650,11 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     // and C2 continues the taken candidate from where C1 stopped
     // (tools/enc_model.c model4, pol 7 vs 0: ratio -0.1 %; measured -0.06 %, -3.4 % VALU).
     const uint32_t eT = eager(X, Y);
+#if APE_LZ4_CAPBITS
+    const uint32_t eL = (umin(first_diff_bit<2, 4>(X, Z), 8u * (kEagerL - 4u)) >> 3) + 4u;
+#else
     const uint32_t eL = umin((first_diff_bit<2, 4>(X, Z) >> 3) + 4u, kEagerL);
+#endif
     const uint32_t lT = okT ? eT : 0u, lL = okL ? eL : 0u;
     const bool pickL = okL & (!okT | ((lT < kEagerL) & (lL >= lT)));
     R.c = pickL ? cL : cT;
