@@ -371,3 +371,56 @@ def test_emitter_batches_mixed(cuda, product, oracle):
         rs2, comps2 = run_encode(cuda, product, srcs, caps=rs, out_mis=mis)
         assert rs2 == rs and comps2 == comps
         assert run_encode(cuda, product, srcs, caps=[r - 1 for r in rs], out_mis=mis)[0] == [0] * len(srcs)
+
+
+def _start_echo_block(seed, n=65536):
+    """Random bytes with a period-3 run at positions 1..11 (broken at 12) whose bytes from
+    position 4 reappear at many interior positions.  Position 1 then sits in the table under
+    the same 5 bytes as every echo, and its 4 bytes of backward context lie before the block:
+    an interior step that took candidate 1 with the bytes of candidate 4 would measure a
+    12-byte match where the true one from position 1 is 8 bytes long."""
+    rng = random.Random(seed)
+    b = bytearray(rng.randbytes(n))
+    b[1:12] = (rng.randbytes(3) * 4)[:11]
+    b[12] = b[9] ^ 0x5A
+    e = bytes(b[4:17])
+    for at in range(300 + seed % 64, n - 200, 997 + 13 * (seed % 7)):
+        b[at:at + len(e)] = e
+    return bytes(b)
+
+
+def test_candidates_at_block_start(cuda, product, oracle):
+    """Table entries for positions 1..3 (their backward context precedes the block) never
+    corrupt a match found by an interior step: blocks that echo their first bytes many times
+    round-trip through the oracle and the GPU decoder."""
+    srcs = [_start_echo_block(s) for s in range(96)]
+    rs, comps = run_encode(cuda, product, srcs)
+    for s, r, c in zip(srcs, rs, comps):
+        assert 0 < r <= product.compressBound(len(s))
+        check_valid(oracle, s, c)
+
+
+def test_many_blocks_gpu_roundtrip(cuda, product):
+    """4096 x 64 KiB App. C blocks and 512 start-echo blocks: GPU encode, GPU decode, every
+    byte compared (a rare bad match shows up at this sample size; the parity tests above
+    decode smaller samples with the reference itself)."""
+    import torch
+    n, nb = 65536, 4096
+    slot = (product.compressBound(n) + 15) // 16 * 16
+    src = torch.empty((nb + 512, n), dtype=torch.uint8, device="cuda")
+    product.synth_blocks(src[:nb], n, 7, 1)
+    src[nb:] = torch.tensor(bytearray(b"".join(_start_echo_block(1000 + s) for s in range(512))),
+                            dtype=torch.uint8).view(512, n).cuda()
+    tot = nb + 512
+    comp = torch.empty((tot, slot), dtype=torch.uint8, device="cuda")
+    out = torch.empty((tot, n), dtype=torch.uint8, device="cuda")
+    sizes = torch.full((tot,), n, dtype=torch.int32, device="cuda")
+    csz = torch.zeros(tot, dtype=torch.int32, device="cuda")
+    dres = torch.zeros(tot, dtype=torch.int32, device="cuda")
+    product.compress_batch(src, sizes, comp, csz)
+    product.decompress_batch(comp, csz, out, dres, dst_caps=sizes)
+    torch.cuda.synchronize()
+    bad = (dres != n).nonzero().flatten().tolist()
+    assert not bad, bad[:8]
+    same = (out == src).all(dim=1)
+    assert bool(same.all()), (~same).nonzero().flatten().tolist()[:8]
