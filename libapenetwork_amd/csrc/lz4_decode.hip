@@ -113,8 +113,10 @@ __device__ __forceinline__ uint4 gload16_nt(gcu8 *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// bytes sh..sh+3 of lo:hi (v_alignbyte; written as a 64-bit shift, the compiler kept later
+// tests on the result in 64 bits)
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
 // Compiler barrier for lane-to-lane communication through LDS inside one wave
