@@ -11,6 +11,12 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 TAG=${1:-r4}
 NB=65536
+# the GPU parity suite and smoke() first (acceleration ratios printed into their own log)
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -20 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu_$TAG.log
+timeout -k 10 200 python -u -m pytest tests/test_gpu_encode.py -m gpu -q -s -k acceleration --timeout 120 --timeout-method thread > gpurun_out/accel_$TAG.log 2>&1 || exit 1
+grep "ratio by acceleration" gpurun_out/accel_$TAG.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail -5 gpurun_out/smoke_$TAG.log; exit 1; }
 bash tools/gpu_bench.sh $TAG || exit 1
 timeout -k 10 400 python3 -u bench.py --sock-chained > gpurun_out/sockc_$TAG.json 2> gpurun_out/sockc_$TAG.err || exit 1
 cat gpurun_out/sockc_$TAG.json
