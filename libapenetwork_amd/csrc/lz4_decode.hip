@@ -269,6 +269,7 @@ struct Spec {
     uint32_t lit, off, ml;
     int ipl, ipo, q;                 // first literal byte, after the offset, next token
     bool fin_in, mlerr, cx;          // input ends in the literals / ml bytes run out / complex
+    bool mlx;                        // match length nibble 15 (an extension byte follows)
 };
 
 template <bool FASTD>
@@ -288,6 +289,7 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
     z.ipo = z.ipl + (int)lit + 2;
     z.fin_in = !FASTD && (uint32_t)z.ipl + lit + 8u > (uint32_t)D.csize;   // ipl >= 1
     const bool mlx = mn == 15u;
+    z.mlx = mlx;
     z.mlerr = !FASTD && mlx && z.ipo + kLastLiterals > D.csize;
     z.cx = lit == 15u || (mlx && e == 255u && !z.mlerr);
     z.ml = mlx ? 15u + e : mn;
@@ -396,7 +398,7 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const Spec z = spec_at<FASTD>(L, D, P, mem ? pos : 0u);
     const uint32_t lit = z.lit, ml = z.ml, off = z.off;
     const int ipl = z.ipl, ipo = z.ipo, q = z.q;
-    const bool fin_in = z.fin_in, mlerr = z.mlerr;
+    const bool fin_in = z.fin_in;
     // output positions, checks in the reference's order
     const uint32_t ob = mem ? (fin_in ? lit : lit + ml + kMinMatch) : 0u;
     const uint32_t ex = wave_excl_scan(ob);
@@ -408,12 +410,22 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const uint32_t iend = (uint32_t)ipl + lit;  // input position after the literals
     // FASTD (:1346-1366 with endOnOutputSize): final once the literals pass cap - 8,
     // valid only when they end exactly at cap; the result is the input consumed
-    const bool fin = FASTD ? (cpy + 8u > ucap)
-                           : (fin_in || (PARTIAL ? ((int64_t)cpy > D.oexit)
-                                                 : (cpy + (uint32_t)kMFLimit > ucap)));
-    const bool badfin = FASTD ? (cpy != ucap)
-                              : (PARTIAL ? (cpy > ucap || iend > (uint32_t)D.csize)
-                                         : (iend != (uint32_t)D.csize || cpy > ucap));
+    // (every condition is a wave mask of single compares: a ballot of an OR / AND of
+    // compares, or a bool kept across a select, was materialised as 0/1 and compared again)
+    uint64_t fm, badfm;   // final sequence; a final one that fails
+    if (FASTD) {
+        fm = wave_ballot(cpy + 8u > ucap);
+        badfm = wave_ballot(cpy != ucap);
+    } else if (PARTIAL) {
+        fm = wave_ballot(fin_in) | wave_ballot((int64_t)cpy > D.oexit);
+        badfm = wave_ballot(cpy > ucap) | wave_ballot(iend > (uint32_t)D.csize);
+    } else {
+        fm = wave_ballot(fin_in) | wave_ballot(cpy + (uint32_t)kMFLimit > ucap);
+        badfm = wave_ballot(iend != (uint32_t)D.csize) | wave_ballot(cpy > ucap);
+    }
+    const bool fin = lane_in(fm);
+    const uint64_t mlm = FASTD ? 0ull
+                               : wave_ballot(z.mlx) & wave_ballot(z.ipo + kLastLiterals > D.csize);
     const bool e_off = (DICT ? cpy + D.dsz : cpy) < off;               // :1375-1376
     // FASTD: the bytes a sequence needs must lie inside the readable bound (the reference
     // has no bound and reads on; here that is an error, never a read past the buffer)
@@ -421,20 +433,27 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
                                     : (uint32_t)q > (uint32_t)D.csize);
     const bool e_cap = cpy + ml + (uint32_t)(kMinMatch + kLastLiterals) > ucap;   // :1444
     // stop = fin || e_off || mlerr || e_cap || e_in; bad = fin ? badfin || e_in : stop
-    const int rv = fin ? ((badfin || e_in) ? -ipl - 1 : (int)(FASTD ? iend : cpy))
-                       : ((e_off || mlerr) ? -ipo - 1 : -q - 1);
     // (ballots of the single conditions, combined as wave masks: no per-lane 0/1)
-    const uint64_t fm = wave_ballot(fin);
-    const uint64_t stm = fm | wave_ballot(e_off) | wave_ballot(mlerr) | wave_ballot(e_cap) |
-                         wave_ballot(e_in);
-    const uint64_t badm = (fm & (wave_ballot(badfin) | wave_ballot(e_in))) | (~fm & stm);
+    const uint64_t om = wave_ballot(e_off) | mlm;   // stops at the offset / ml bytes
+    const uint64_t inm = FASTD ? wave_ballot(e_in) : 0ull;
+    const uint64_t stm = fm | om | wave_ballot(e_cap) | inm;
+    const uint64_t badm = (fm & (badfm | inm)) | (~fm & stm);
     const uint64_t sm = M & stm;
     uint64_t emit = M;
     int st = ST_MORE;
     if (sm) {
         const int T = __ffsll((long long)sm) - 1;
-        res = (int)lane_val((uint32_t)rv, T);
         const bool tbad = (badm >> T) & 1ull;
+        // the result of the stopping sequence T, formed only here (a per-lane select chain
+        // on every pass had become a divergent branch that re-materialised the masks):
+        // final: bad ? -(ip)-1 : output size (FASTD: input consumed); otherwise -(ip)-1 at
+        // the offset / ml bytes or after the sequence
+        if ((fm >> T) & 1ull)
+            res = tbad ? -(int)lane_val((uint32_t)ipl, T) - 1
+                       : (int)lane_val(FASTD ? iend : cpy, T);
+        else
+            res = ((om >> T) & 1ull) ? -(int)lane_val((uint32_t)ipo, T) - 1
+                                     : -(int)lane_val((uint32_t)q, T) - 1;
         // members before T (error) or up to T (final literals)
         emit = tbad ? ((1ull << T) - 1ull) : ((2ull << T) - 1ull);   // T <= 43
         st = tbad ? ST_ERR : ST_DONE;
