@@ -648,41 +648,48 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
     const uint32_t nm = mb > ma ? mb - ma : 0u;
     const uint32_t off = q.off;
     const int ps = (int)ma - (int)off;
+    // Every condition below is a wave mask of single compares (a ballot of an AND / OR of
+    // compares, or a bool kept across a select, was materialised as 0/1 and compared again).
     // literal: lane path when short and staged
     const uint32_t rs = lsrc - (uint32_t)D.s0;
-    const bool litL = nl != 0u && nl <= 16u && rs < (uint32_t)kStage && rs + nl <= (uint32_t)kStage;
+    const uint64_t nlm = wave_ballot(nl != 0u);
+    const uint64_t litm = nlm & wave_ballot(nl <= 16u) & wave_ballot(rs < (uint32_t)kStage) &
+                          wave_ballot(rs + nl <= (uint32_t)kStage);
     // match: lane path (window / dst history / dictionary sources, or a self-overlap with
     // offset >= 16 inside the window; a match cut by a segment edge can be shorter than 4)
     // or the whole wave; pe = end of the sources it needs from this segment
-    const bool ovl = off != 0u && off < nm;
+    const uint64_t off0m = wave_ballot(off == 0u);
+    const uint64_t ovlm = ~off0m & wave_ballot(off < nm);
     const int pe0 = ps + (int)nm;
-    const bool inw = ps >= (int)base;
-    const bool ing = (!DICT || ps >= 0) && pe0 <= (int)W.gdone && (nm >= 16u || ps + 16 <= D.cap);
-    const bool ind = DICT && ps + (int)umax(nm, 16u) <= 0;
-    const bool lp_n = inw || ing || ind;
-    const bool lp_o = off >= 16u && inw;
-    const bool lp = nm >= 4u && nm <= kLaneMax && (off == 0u || (ovl ? lp_o : lp_n));
-    const bool glb = off != 0u && !inw;
-    const int pe = off == 0u ? -0x7FFFFFFF : (ovl ? (int)ma : pe0);
-    bool mpend = nm != 0u;
+    const uint64_t inwm = wave_ballot(ps >= (int)base);
+    uint64_t ingm = wave_ballot(pe0 <= (int)W.gdone) &
+                    (wave_ballot(nm >= 16u) | wave_ballot(ps + 16 <= D.cap));
+    if (DICT) ingm &= wave_ballot(ps >= 0);
+    const uint64_t indm = DICT ? wave_ballot(ps + (int)umax(nm, 16u) <= 0) : 0ull;
+    const uint64_t lpnm = inwm | ingm | indm;
+    const uint64_t lpom = wave_ballot(off >= 16u) & inwm;
+    const uint64_t lpm = wave_ballot(nm >= 4u) & wave_ballot(nm <= kLaneMax) &
+                         (off0m | (ovlm & lpom) | (~ovlm & lpnm));
+    const bool glb = lane_in(~off0m & ~inwm);
+    const int pe = lane_in(off0m) ? -0x7FFFFFFF : (lane_in(ovlm) ? (int)ma : pe0);
+    const uint64_t mpm = wave_ballot(nm != 0u);
 
     // literals
-    for (uint64_t lc = wave_ballot(nl != 0u && !litL); lc; lc &= lc - 1ull) {
+    for (uint64_t lc = nlm & ~litm; lc; lc &= lc - 1ull) {
         const int f = __builtin_ctzll(lc);
         coop_literal(L, D, base, lane_val(la, f), lane_val(nl, f), lane_val(lsrc, f));
     }
     wave_sync();
-    if (litL) {
+    if (lane_in(litm)) {
         uint8_t *w = L.win + (la - base);
         const uint4 v = lds16(L.stage + rs);
         if (nl == 16u) lds_st16(w, v);
         else lds_put_small<false>(w, v, nl);
     }
     // round 1
-    const bool r1 = mpend && lp && pe <= (int)S0;
-    lane_match<DICT>(L, D, base, r1, ma, nm, off, glb);
-    mpend = mpend && !r1;
-    uint64_t pm = wave_ballot(mpend);
+    const uint64_t r1m = mpm & lpm & wave_ballot(pe <= (int)S0);
+    lane_match<DICT>(L, D, base, lane_in(r1m), ma, nm, off, glb);
+    uint64_t pm = mpm & ~r1m;
     if (!pm) return;
     // sequences owning [max(ps, S0), pe): k0 = owner(first byte), k1 = owner(last byte),
     // by binary search over the sequence starts (lanes past the batch hold B1)
@@ -696,12 +703,9 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
         k1 = v1 <= x1 ? c1 : k1;
     }
     k1 = umin(k1, (uint32_t)lane - 1u);   // (its own literal is written; lane 0 has no needs)
-    const uint64_t need = (mpend && lane > 0 && k0 <= k1)
+    const uint64_t need = (lane_in(pm) && lane > 0 && k0 <= k1)
                               ? (((2ull << k1) - 1ull) & ~((1ull << k0) - 1ull)) : 0ull;
-    uint64_t done = ~pm;
-    // lanes still pending = pm & ~done; kept as wave masks (a ballot of compares folds into
-    // the compares; a ballot of a combined bool made the compiler materialise a 0/1)
-    const uint64_t lpm = wave_ballot(lp);
+    uint64_t done = ~pm;   // lanes still pending = pm & ~done
     wave_sync();
     for (;;) {
         diag += 1u;

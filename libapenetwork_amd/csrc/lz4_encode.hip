@@ -460,9 +460,12 @@ struct Blk {
 
 // ---------------- producer ----------------
 struct Part {                        // C1 result of one chunk, finished by C2
-    uint32_t len, c, bk, lim, h, base;   // base: bytes C1 measured (kEagerLen / kEagerL)
+    uint32_t len, c, bk, lim, base;      // base: bytes C1 measured (kEagerLen / kEagerL)
+    uint32_t iy;                     // info.y: offset (0 = no candidate) | h << 16, formed in C1
+                                     // while `has` is a lane mask (a bool carried to C2 was
+                                     // materialised as 0/1 and compared again)
     uint32_t rank, ntr, eo;          // stage-2 queue rank, queue size, own bytes of the group
-    bool has, hashable;
+    bool hashable;
     uint64_t tmask;                  // lanes whose candidate reached its measured length (a
                                      // wave mask: no per-lane 0/1 to materialise)
     uint64_t smask;                  // ... of them, the lanes stage 2 measures
@@ -680,8 +683,7 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     R.smask = R.tmask;
 #endif
     R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
-    R.has = okT | okL;
-    R.h = h;
+    R.iy = ((okT | okL) ? p - R.c : 0u) | (h << 16);
 #undef Y
 }
 
@@ -741,7 +743,7 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
     // chunk when the first step is FAST)
     S.info[lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
                                   ((FAST || R.hashable) ? I_HASHABLE : 0u),
-                                     (R.has ? p - R.c : 0u) | (R.h << 16));
+                                     R.iy);
 }
 
 // ---------------- walker ----------------
