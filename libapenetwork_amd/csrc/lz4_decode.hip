@@ -372,7 +372,11 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     int cntA;
     chain_at<FASTD>(L, D, P, posA, cntA, XA, lastA);
     const bool cplxA = XA == kHopCplx;
-    const int nmA = cplxA ? cntA - 1 : cntA;   // the complex token is not a member
+    // the complex token is not a member.  (XA is wave-uniform and is 64..84, kHopTerm 0x80 or
+    // kHopCplx 0xC0: bits 7 and 6 both set only for kHopCplx -- scalar arithmetic, where a
+    // select on the bool was materialised in a VGPR)
+    static_assert(kHopCplx == 0xC0u && kHopTerm == 0x80u, "hop exit codes");
+    const int nmA = cntA - (int)((XA >> 7) & (XA >> 6) & 1u);
     const int PB = P + (int)XA;
     const bool two = XA < kHopTerm && PB - D.s0 + kWinNeed <= kStage;
     int nmB = 0, Pn;
@@ -382,7 +386,7 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
         int cntB;
         chain_at<FASTD>(L, D, PB, posB, cntB, XB, lastB);
         cplx = XB == kHopCplx;
-        nmB = cplx ? cntB - 1 : cntB;
+        nmB = cntB - (int)((XB >> 7) & (XB >> 6) & 1u);   // (as nmA)
         Pn = PB + (int)(XB >= kHopTerm ? lastB : XB);   // (not past a final token)
     } else {
         cplx = cplxA;

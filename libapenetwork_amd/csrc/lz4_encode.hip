@@ -1068,7 +1068,7 @@ __device__ __forceinline__ void emit_fetch(EncLds &S, const Blk &B, int lane, Em
     const uint32_t size = v0 ? 3u + ext_bytes(lit) + lit + ext_bytes(mlm4) : 0u;
     const uint32_t isz = wave_incl_sum(size);
     // the leading records that fit the staging buffer (at least one)
-    const uint32_t nrec = umax((uint32_t)__popcll(wave_ballot(v0 && isz <= kStage)), 1u);
+    const uint32_t nrec = umax((uint32_t)__popcll(wave_ballot(v0) & wave_ballot(isz <= kStage)), 1u);
     const bool v = (uint32_t)lane < nrec;
     const uint32_t adv = v ? lit + mlm4 + kMinMatch : 0u;
     const uint32_t iadv = wave_incl_sum(adv);
