@@ -624,8 +624,16 @@ ChainPart *part_new(int nconn, int msg_len, int dev) {
     c->nt = nconn * c->K * c->nch;
     c->W = ((size_t)2 * kHist + (size_t)c->K * msg_len + 255) & ~(size_t)255;
     const size_t nt = (size_t)c->nt, fr = nt * (kChunkSlot + 4) + 64;
-    bool ok = hipStreamCreateWithFlags(&c->tst, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&c->rst, hipStreamNonBlocking) == hipSuccess;
+    // RX at the highest stream priority, TX at the lowest: the receive side is a chain of small
+    // dependent launches (one per chunk position, each one chunk per connection) whose latency
+    // bounds the connection's rate, while the TX launch of a round is one large batch; the
+    // parts' streams share the device's hardware queues (APE_LZ4_CHAIN_PRIO=0: default priority)
+    int lo = 0, hi = 0;   // numerically: lo = least, hi = greatest priority
+    const char *pe = getenv("APE_LZ4_CHAIN_PRIO");
+    if (!(pe && atoi(pe) == 0) && hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+    if (pe && atoi(pe) == 0) lo = hi = 0;
+    bool ok = hipStreamCreateWithPriority(&c->tst, hipStreamNonBlocking, lo) == hipSuccess &&
+              hipStreamCreateWithPriority(&c->rst, hipStreamNonBlocking, hi) == hipSuccess;
     for (int b = 0; b < 2 && ok; b++)
         ok = hipEventCreateWithFlags(&c->tev[b], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->rev[b], hipEventDisableTiming) == hipSuccess &&
