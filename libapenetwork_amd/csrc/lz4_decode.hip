@@ -808,13 +808,10 @@ __device__ __forceinline__ void copy_batch(WaveLds &L, const Dec &D, Win &W, int
 
 }  // namespace
 
+// One block (block index b of the batch) decoded by the calling wave.
 template <bool PARTIAL, bool DICT, bool FASTD>
-__global__ void __launch_bounds__(64)
-lz4_decode_kernel(BlockArgs a) {
-    __shared__ WaveLds L;
-    const int b = blockIdx.x;
-    const int lane = threadIdx.x;
-
+__device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, const int b,
+                                             const int lane) {
     Dec D;
     D.dst = (gu8 *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
     if (a.frame_off) {   // framed stream: [le32 size][block] (lz4_frame.hip)
@@ -949,6 +946,29 @@ lz4_decode_kernel(BlockArgs a) {
     if (lane == 0) a.result[b] = result;
     STAT_ADD(10, 1);
     STATS_FLUSH(g_dec_stats);
+}
+
+template <bool PARTIAL, bool DICT, bool FASTD>
+__global__ void __launch_bounds__(64)
+lz4_decode_kernel(BlockArgs a) {
+    __shared__ WaveLds L;
+    decode_block<PARTIAL, DICT, FASTD>(L, a, (int)blockIdx.x, (int)threadIdx.x);
+}
+
+// Chained streams (lz4_sock.hip): workgroup i decodes chunks i, i + nconn, i + 2 nconn, ...
+// in order -- chunk q + 1 of a connection takes the output of chunks <= q as its dictionary
+// -- so a round of nq chunk positions is one launch instead of nq.  Between chunks, the
+// wave's stores are made visible to its own loads (release, then acquire with the L1
+// invalidated).
+__global__ void __launch_bounds__(64)
+lz4_decode_chain_kernel(BlockArgs a, int nconn, int nq) {
+    __shared__ WaveLds L;
+    for (int q = 0; q < nq; q++) {
+        decode_block<false, true, false>(L, a, q * nconn + (int)blockIdx.x, (int)threadIdx.x);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
 }
 
 #ifdef APE_LZ4_DEC_COOP
@@ -1088,6 +1108,12 @@ lz4_decode_coop_kernel(BlockArgs a) {
     }
 }
 #endif
+
+hipError_t launch_decode_chain(const BlockArgs &a, int nconn, int nq, hipStream_t s) {
+    if (nconn <= 0 || nq <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lz4_decode_chain_kernel, dim3(nconn), dim3(64), 0, s, a, nconn, nq);
+    return hipGetLastError();
+}
 
 hipError_t launch_decode(const BlockArgs &a, bool partial, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;

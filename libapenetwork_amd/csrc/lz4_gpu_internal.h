@@ -142,6 +142,9 @@ struct BlockArgs {
 };
 
 hipError_t launch_decode(const BlockArgs &a, bool partial, hipStream_t s);
+// usingDict decodes of nq chunk positions x nconn connections (block q * nconn + i), one
+// workgroup per connection looping over its chunks in order (lz4_decode.hip)
+hipError_t launch_decode_chain(const BlockArgs &a, int nconn, int nq, hipStream_t s);
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s);
 // compress_destSize pass 2 (lz4_destsize.hip): scratch slot i (at scratch + i*stride, encoder
 // result sres[i]) -> dst[i] cut to target[i]; src_size[i] <- consumed input

@@ -535,6 +535,8 @@ __global__ void chain_rx_setup(const char *stage, const long long *poff, char *w
 // streams and buffers (APE_LZ4_chain below splits the connections over kChainThreads parts).
 struct ChainPart {
     int dev = 0, nconn = 0, msg = 0, nch = 0, K = 1, nt = 0;   // nt = chunks of a full round
+    bool loop = true;                // RX: one looping launch per round (APE_LZ4_CHAIN_LOOP=0: one
+                                     // launch per chunk position)
     size_t W = 0;
     // TX (one thread): device window, compressed slots, frames, pointer arrays
     hipStream_t tst = nullptr;
@@ -621,6 +623,7 @@ ChainPart *part_new(int nconn, int msg_len, int dev) {
         const int k = atoi(ev);
         if (k >= 1 && k <= 64) c->K = k;
     }
+    if (const char *ev = getenv("APE_LZ4_CHAIN_LOOP")) c->loop = atoi(ev) != 0;
     c->nt = nconn * c->K * c->nch;
     c->W = ((size_t)2 * kHist + (size_t)c->K * msg_len + 255) & ~(size_t)255;
     const size_t nt = (size_t)c->nt, fr = nt * (kChunkSlot + 4) + 64;
@@ -850,11 +853,25 @@ long long part_recv(ChainPart *c, const int *fds, char *h_out, size_t out_stride
                            c->rpoff[b], c->rxwin, c->W, c->rxpos, c->msg, nch, k, M, c->rsrc, c->rdst,
                            c->rcap, c->rdict, c->rdsz);
         if (hipGetLastError() != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
-        for (int q = 0; q < nf && rc == 0; q++) {
-            const size_t e0 = (size_t)q * M;
-            rc = APE_LZ4_decompress_safe_usingDict_batch_dev(c->rsrc + e0, c->rcsz[b] + e0, c->rdst + e0,
-                                                             c->rcap + e0, c->rdict + e0, c->rdsz + e0,
-                                                             c->rres[b] + e0, M, c->rst);
+        if (c->loop) {   // one launch: workgroup i decodes connection i's nf chunks in order
+            BlockArgs a{};
+            a.src = c->rsrc;
+            a.src_size = c->rcsz[b];
+            a.dst = c->rdst;
+            a.dst_cap = c->rcap;
+            a.dict = c->rdict;
+            a.dict_size = c->rdsz;
+            a.result = c->rres[b];
+            a.nblocks = ne;
+            if (apelz4::launch_decode_chain(a, M, nf, c->rst) != hipSuccess) rc = APE_LZ4_GPU_ELAUNCH;
+        } else {         // a usingDict launch per chunk position
+            for (int q = 0; q < nf && rc == 0; q++) {
+                const size_t e0 = (size_t)q * M;
+                rc = APE_LZ4_decompress_safe_usingDict_batch_dev(c->rsrc + e0, c->rcsz[b] + e0,
+                                                                 c->rdst + e0, c->rcap + e0,
+                                                                 c->rdict + e0, c->rdsz + e0,
+                                                                 c->rres[b] + e0, M, c->rst);
+            }
         }
         if (rc) break;
         for (int mm = 0; mm < k && e == hipSuccess; mm++)
