@@ -397,16 +397,19 @@ def test_chain_gpu_tx_decoded_by_reference(cuda, product, monkeypatch, msg_len, 
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("msg_len,nmsg,pieces,per_round", [(65536, 6, False, 0), (65536, 7, False, 2),
-                                                           (25576, 4, True, 3)])
+@pytest.mark.parametrize("msg_len,nmsg,pieces,per_round,loop", [
+    (65536, 6, False, 0, 1), (65536, 7, False, 2, 1), (25576, 4, True, 3, 1),
+    (65536, 7, True, 2, 0)])
 def test_chain_reference_tx_decoded_by_gpu(cuda, product, monkeypatch, msg_len, nmsg, pieces,
-                                           per_round):
+                                           per_round, loop):
     """GPU chain_recv reads the reference's wire format: frames from the reference's own
     compress_fast_continue + saveDict (ape_socket.c:811-871) decode bit-exactly -- in one round
     and in rounds of 2-3 messages (window slides, a partial last round) -- also when the sender
-    writes them in 1-7-byte and random pieces (every header split: the K7 parser)."""
+    writes them in 1-7-byte and random pieces (every header split: the K7 parser); with the
+    looping decode (one launch per round, the default) and with a launch per chunk position."""
     if per_round:
         monkeypatch.setenv("APE_LZ4_CHAIN_ROUND", str(per_round))
+    monkeypatch.setenv("APE_LZ4_CHAIN_LOOP", str(loop))
     nconn = 4
     peer = _ref_peer()
     msgs = _chain_msgs(cuda, product, nmsg, nconn, msg_len, seed=msg_len + 1)
