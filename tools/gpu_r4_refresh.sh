@@ -18,6 +18,9 @@ timeout -k 10 200 python -u -m pytest tests/test_gpu_encode.py -m gpu -q -s -k a
 grep "ratio by acceleration" gpurun_out/accel_$TAG.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail -5 gpurun_out/smoke_$TAG.log; exit 1; }
 bash tools/gpu_bench.sh $TAG || exit 1
+# config-4 self-launch rehearsal: two ranks of `bench.py --gpus 2` on the one device
+APE_BENCH_DEVICE=0 timeout -k 10 400 python3 -u bench.py --gpus 2 --blocks 131072 > gpurun_out/rehearse2_$TAG.json 2> gpurun_out/rehearse2_$TAG.err || { tail -5 gpurun_out/rehearse2_$TAG.err; exit 1; }
+cat gpurun_out/rehearse2_$TAG.json
 timeout -k 10 400 python3 -u bench.py --sock-chained > gpurun_out/sockc_$TAG.json 2> gpurun_out/sockc_$TAG.err || exit 1
 cat gpurun_out/sockc_$TAG.json
 bash tools/sq_passes.sh 16384 > gpurun_out/sq_$TAG.txt 2>&1 || { tail -5 gpurun_out/sq_$TAG.txt; exit 1; }
