@@ -136,6 +136,9 @@ static_assert(kFetchAt < kEmitAll, "a fetch precedes emit_all");
 #ifndef APE_LZ4_ACC_L
 #define APE_LZ4_ACC_L 1
 #endif
+#ifndef APE_LZ4_APF
+#define APE_LZ4_APF 1                // producer: own-bytes load A two steps ahead (else one)
+#endif
 #ifndef APE_LZ4_CAPBITS
 #define APE_LZ4_CAPBITS 1            // length caps folded into the bit-index mins (v_min3)
 #endif
@@ -1266,7 +1269,8 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             // Every stage runs on every step, past the last chunk too (it then loads
             // from the block start and records nothing), so the number of loads per
             // step -- and with it the waits -- is the same on every path.
-            // In flight, oldest first: A(s+2), Y(s+1) x2, E(s) -> A(s+2) at 3.
+            // In flight, oldest first: A(s+2), Y(s+1), A(s+3), E(s) -> A(s+2) at 3 (APF; without:
+            // A(s+2), Y(s+1), E(s)).
             vm_wait<kWin ? 0 : 3>();
             STAT(9);   // (stats build: load waits)
             // ring copy of chunk s+2 (loaded a step ago), then C1(s+1)'s own bytes (chunks
@@ -1276,9 +1280,18 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             prod_ring<F>(S, B, s + 2, lane, cur.X);
             uint32_t X6[6];   // C1(s+1)'s own bytes: in the ring since last step, read first
             prod_own(S, s + 1, lane, X6);
+#if APE_LZ4_APF
+            prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
+            // A two steps ahead, into the set B(s+2) has just consumed: the block's own input
+            // streams in from HBM, and one step (~1 us) did not cover it (the producer's load
+            // waits were the A load at the step start)
+            prod_load<SMALL, F>(B, s + 4, lane, cur.X);
+            // Y(s+1), A(s+3), E(s), Y(s+2), A(s+4) -> Y(s+1) at 4
+#else
             prod_load<SMALL, F>(B, s + 3, lane, nxt.X);
             prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
             // Y(s+1) x2, E(s), A(s+3), Y(s+2) x2 -> Y(s+1) at 4
+#endif
             STAT(5);
             vm_wait<kWin ? 1 : 4>();
             STAT(9);
@@ -1306,7 +1319,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             // E(s), A(s+3), Y(s+2) x2, E(s+1) -> E(s) at 4 (A(s+3), issued half a step ago,
             // is not needed before the next step)
             STAT(7);
-            vm_wait<kWin ? 0 : 4>();
+            vm_wait<kWin ? 0 : (APE_LZ4_APF ? 3 : 4)>();   // (APF: Y(s+2), A(s+4), E(s+1) after E(s))
             STAT(9);
             prod_finish<SMALL, F>(S, B, s, lane, cur.q, cur.E);
             STAT(7);
@@ -1322,6 +1335,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             prod_load<SMALL>(B, k0 + 2, lane, P0.X);
             prod_ring(S, B, k0 + 1, lane, P1.X);
             prod_lookup<SMALL>(S, B, k0 + 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
+            if (APE_LZ4_APF) prod_load<SMALL>(B, k0 + 3, lane, P1.X);   // (step k0 + 1's X)
             prod_ring(S, B, k0 + 2, lane, P0.X);
             uint32_t X6[6];
             prod_own(S, k0, lane, X6);
@@ -1335,7 +1349,9 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         // Steps whose three loads all lie inside the block (A(s+3): 64(s+3)+72 <= n,
         // Y(s+2): 64(s+2)+83, E(s+1): 64(s+1)+148) run a loop without the edge paths;
         // the last few steps run the general one.
-        const int nfast_abs = SMALL ? 0 : (int)umin((uint32_t)(B.n >= 264 ? (B.n - 264) / 64 + 1 : 0),
+        // (APF: A(s+4), 64(s+4)+72 <= n)
+        constexpr int kFastEnd = APE_LZ4_APF ? 328 : 264;
+        const int nfast_abs = SMALL ? 0 : (int)umin((uint32_t)(B.n >= kFastEnd ? (B.n - kFastEnd) / 64 + 1 : 0),
                                                     (uint32_t)nsteps);
         const int nfast = nfast_abs > k0 ? k0 + ((nfast_abs - k0) & ~1) : k0;
         int s = k0;
