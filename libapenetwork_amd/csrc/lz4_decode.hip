@@ -59,8 +59,11 @@ static_assert(kKeep >= 64 && kKeep % 16 == 0 && kWinB >= kKeep + 1024 && kWinB %
 constexpr int kStage = APE_LZ4_DSTAGE;   // staged compressed bytes (a multiple of 256)
 constexpr int kWinNeed = 84;     // a parse window reads up to P + 63 + 21
 constexpr int kBatch = 64;       // descriptors per copy batch (one per lane)
-constexpr int kMaxDesc = kBatch + 44;   // held before a copy: <= 63, + <= 44 per parse step, + 1
+constexpr int kMaxDesc = kBatch + 44;   // held before a copy: <= 63 + 44 (two windows); a third only while nd stays <= kMaxDesc
 constexpr uint32_t kLaneMax = 64;  // longest match one lane copies (4 x 16 bytes)
+#ifndef APE_LZ4_DWIN3
+#define APE_LZ4_DWIN3 1            // up to three speculative windows per member pass
+#endif
 #ifndef APE_LZ4_DUNITS
 #define APE_LZ4_DUNITS 1           // lane matches load / store only the 16-byte units they need
 #endif
@@ -358,8 +361,9 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
     lastp = lane_val(pos, cnt - 1);
 }
 
-// Up to two speculative windows (P, then where the first one's chain leaves it, if that
-// is staged) and one pass over their members: appends the descriptors (<= 44).  Returns
+// Up to three speculative windows (P, then where each chain leaves the last, if that is
+// staged and the members fit) and one pass over their members: appends the descriptors
+// (<= 63, and nd stays <= kMaxDesc).  Returns
 // ST_MORE with P advanced (to the next token, or to a complex token when `cplx`), or
 // ST_DONE / ST_ERR with `res`.  Members are lanes [0, nm) in chain order: lane t re-reads
 // its sequence from the staged bytes.
@@ -379,24 +383,49 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const int nmA = cntA - (int)((XA >> 7) & (XA >> 6) & 1u);
     const int PB = P + (int)XA;
     const bool two = XA < kHopTerm && PB - D.s0 + kWinNeed <= kStage;
-    int nmB = 0, Pn;
-    uint32_t posB = 0;
+    int nmB = 0, nmC = 0, Pn, PC = PB;
+    uint32_t posB = 0, posC = 0;
     if (two) {
         uint32_t XB, lastB;
         int cntB;
         chain_at<FASTD>(L, D, PB, posB, cntB, XB, lastB);
-        cplx = XB == kHopCplx;
         nmB = cntB - (int)((XB >> 7) & (XB >> 6) & 1u);   // (as nmA)
-        Pn = PB + (int)(XB >= kHopTerm ? lastB : XB);   // (not past a final token)
+        PC = PB + (int)XB;
+#if APE_LZ4_DWIN3
+        // a third window while the members still fit the wave (<= 41 + 22 lanes) and the
+        // descriptors the array (nd + nm <= kMaxDesc), and its bytes are staged
+        const bool three = XB < kHopTerm && nmA + nmB <= 41 && nd + nmA + nmB <= kMaxDesc - 22 &&
+                           PC - D.s0 + kWinNeed <= kStage;
+#else
+        const bool three = false;
+#endif
+        if (three) {
+            uint32_t XC, lastC;
+            int cntC;
+            chain_at<FASTD>(L, D, PC, posC, cntC, XC, lastC);
+            cplx = XC == kHopCplx;
+            nmC = cntC - (int)((XC >> 7) & (XC >> 6) & 1u);
+            Pn = PC + (int)(XC >= kHopTerm ? lastC : XC);
+        } else {
+            cplx = XB == kHopCplx;
+            Pn = PB + (int)(XB >= kHopTerm ? lastB : XB);   // (not past a final token)
+        }
     } else {
         cplx = cplxA;
         Pn = P + (int)(XA >= kHopTerm ? lastA : XA);
     }
     const uint32_t pB = bperm(posB, (t - (uint32_t)nmA) & 63u);
-    const int nm = nmA + nmB;
-    const uint64_t M = (1ull << nm) - 1ull;   // nm <= 44
+    const int nmAB = nmA + nmB;
+    const int nm = nmAB + nmC;
+    const uint64_t M = (1ull << nm) - 1ull;   // nm <= 63
     const bool mem = (int)t < nm;
-    const uint32_t pos = (int)t < nmA ? posA : (uint32_t)(PB - P) + pB;   // relative to P
+    uint32_t pos = (int)t < nmA ? posA : (uint32_t)(PB - P) + pB;   // relative to P
+#if APE_LZ4_DWIN3
+    if (nmC) {
+        const uint32_t pC = bperm(posC, (t - (uint32_t)nmAB) & 63u);
+        pos = (int)t < nmAB ? pos : (uint32_t)(PC - P) + pC;
+    }
+#endif
 
     // member t = the sequence at P + pos, re-read from the staged bytes
     const Spec z = spec_at<FASTD>(L, D, P, mem ? pos : 0u);
@@ -459,7 +488,7 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
             res = ((om >> T) & 1ull) ? -(int)lane_val((uint32_t)ipo, T) - 1
                                      : -(int)lane_val((uint32_t)q, T) - 1;
         // members before T (error) or up to T (final literals)
-        emit = tbad ? ((1ull << T) - 1ull) : ((2ull << T) - 1ull);   // T <= 43
+        emit = tbad ? ((1ull << T) - 1ull) : ((2ull << T) - 1ull);   // T <= 62
         st = tbad ? ST_ERR : ST_DONE;
         cplx = false;
     }
@@ -884,7 +913,7 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
         return;
     }
 
-    // Per batch: parse until >= 64 descriptors are held (a parse step adds <= 44), then
+    // Per batch: parse until >= 64 descriptors are held (nd <= kMaxDesc after a step), then
     // produce the output of the first 64 through the LDS window (copy_batch) and carry
     // the rest.  A failing sequence ends the block without copying its batch (the result
     // is the error; dst bytes are unspecified then).
