@@ -61,6 +61,9 @@ constexpr int kWinNeed = 84;     // a parse window reads up to P + 63 + 21
 constexpr int kBatch = 64;       // descriptors per copy batch (one per lane)
 constexpr int kMaxDesc = kBatch + 44;   // held before a copy: <= 63 + 44 (two windows); a third only while nd stays <= kMaxDesc
 constexpr uint32_t kLaneMax = 64;  // longest match one lane copies (4 x 16 bytes)
+#ifndef APE_LZ4_DMUX
+#define APE_LZ4_DMUX 1             // chain_at's lane-bit selects as VGPR-mask muxes (v_bfi)
+#endif
 #ifndef APE_LZ4_DWIN3
 #define APE_LZ4_DWIN3 1            // up to three speculative windows per member pass
 #endif
@@ -195,6 +198,9 @@ struct Dec {
     int64_t oexit;
     int s0;          // staged window start
     int lane;
+#if APE_LZ4_DMUX
+    uint32_t mk[5];  // mk[k]: all ones on lanes with bit k set (chain_at's lifting selects, VGPRs)
+#endif
 };
 
 enum { ST_MORE = 0, ST_DONE = 1, ST_ERR = 2 };
@@ -258,6 +264,13 @@ __device__ int parse_scalar(WaveLds &L, const Dec &D, int &ip, uint32_t &op, int
     nd++;
     op = (uint32_t)mend;
     return ST_MORE;
+}
+
+// bitwise m ? a : b (v_bfi_b32)
+__device__ __forceinline__ uint32_t vmux(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
 }
 
 // lane l receives v of lane idx (0..63)
@@ -329,6 +342,24 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
     const uint32_t J2 = jump(J1, J1);
     const uint32_t J3 = jump(J2, J2);
     const uint32_t t = (uint32_t)D.lane;
+#if APE_LZ4_DMUX
+    // lane t takes J_k where bit k of t is set: a v_bfi on a per-lane VGPR mask each (the
+    // lane masks had been hoisted into SGPR pairs, and the SGPR file spilled them to VGPR
+    // lanes: two v_readlane to reload one, inside the parse loop)
+    uint32_t p = vmux(D.mk[0], lane_val(hop, 0), 0u);
+    p = vmux(D.mk[1], jump(J1, p), p);
+    p = vmux(D.mk[2], jump(J2, p), p);
+    p = vmux(D.mk[3], jump(J3, p), p);
+    const uint32_t p15 = lane_val(p, 15);
+    // lanes 16..31 take J^16, or the exit p15 when the chain has no member 15 (lanes >= 32
+    // are no members); J^16 and its two dependent rounds only when needed (wave-uniform)
+    uint32_t sel = p15;
+    if (p15 < 256u) {
+        const uint32_t J4 = jump(J3, J3);
+        sel = jump(J4, p);
+    }
+    p = vmux(D.mk[4], sel, p);
+#else
     uint32_t p = (t & 1u) ? lane_val(hop, 0) : 0u;
     const uint32_t p2 = jump(J1, p);
     p = (t & 2u) ? p2 : p;
@@ -353,6 +384,7 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
     const uint32_t J4 = jump(J3, J3);
     const uint32_t p16 = jump(J4, p);
     p = (t & 16u) ? p16 : p;
+#endif
 #endif
     p >>= 2;
     pos = t < 32u ? p : kHopTerm;
@@ -868,6 +900,13 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
     D.oexit = PARTIAL ? a.target[b] : 0;
     if (PARTIAL && D.oexit > (int64_t)D.cap - kMFLimit) D.oexit = (int64_t)D.cap - kMFLimit;
     D.lane = lane;
+#if APE_LZ4_DMUX
+    for (int k = 0; k < 5; ++k) {
+        uint32_t m = 0u - (((uint32_t)lane >> k) & 1u);
+        asm volatile("" : "+v"(m));   // opaque: stays a VGPR mask, not turned back into a select
+        D.mk[k] = m;
+    }
+#endif
     D.dend = nullptr;
     D.dsz = 0;
     if (DICT) {   // usingDict (:1625-1647): any placement, adjacent or not, reads the same
@@ -1040,6 +1079,13 @@ lz4_decode_coop_kernel(BlockArgs a) {
     D.oexit = PARTIAL ? a.target[b] : 0;
     if (PARTIAL && D.oexit > (int64_t)D.cap - kMFLimit) D.oexit = (int64_t)D.cap - kMFLimit;
     D.lane = lane;
+#if APE_LZ4_DMUX
+    for (int k = 0; k < 5; ++k) {
+        uint32_t m = 0u - (((uint32_t)lane >> k) & 1u);
+        asm volatile("" : "+v"(m));   // opaque: stays a VGPR mask, not turned back into a select
+        D.mk[k] = m;
+    }
+#endif
     D.dend = nullptr;
     D.dsz = 0;
     if (DICT) {
