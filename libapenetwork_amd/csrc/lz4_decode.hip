@@ -711,7 +711,10 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
     const uint32_t lsrc = q.ls + (la - q.o);
     const uint32_t ma = umax(q.m, S0), mb = umin(q.me, S1);
     const uint32_t nm = mb > ma ? mb - ma : 0u;
-    const uint32_t off = q.off;
+    uint32_t off = q.off;
+    // opaque per segment: compares on it stay here (the loop-invariant ones, hoisted out of
+    // the segment loop, were kept as per-lane bools and re-materialised as 0/1 + v_cmp)
+    asm volatile("" : "+v"(off));
     const int ps = (int)ma - (int)off;
     // Every condition below is a wave mask of single compares (a ballot of an AND / OR of
     // compares, or a bool kept across a select, was materialised as 0/1 and compared again).
