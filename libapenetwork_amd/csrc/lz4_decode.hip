@@ -64,6 +64,12 @@ constexpr uint32_t kLaneMax = 64;  // longest match one lane copies (4 x 16 byte
 #ifndef APE_LZ4_DMUX
 #define APE_LZ4_DMUX 1             // chain_at's lane-bit selects as VGPR-mask muxes (v_bfi)
 #endif
+#ifndef APE_LZ4_DREL
+#define APE_LZ4_DREL 1             // spec compares on staged positions, one b64 read, hop alone
+#endif
+#ifndef APE_LZ4_DJMAX
+#define APE_LZ4_DJMAX 1            // lifting jumps absorb exits with a max
+#endif
 #ifndef APE_LZ4_DWIN3
 #define APE_LZ4_DWIN3 1            // up to three speculative windows per member pass
 #endif
@@ -72,8 +78,9 @@ constexpr uint32_t kLaneMax = 64;  // longest match one lane copies (4 x 16 byte
 #endif
 
 struct __attribute__((aligned(16))) WaveLds {
-    uint8_t win[kWinB + 64];     // output [base, base + kWinB) (+ slack for 16-byte reads)
+    // stage first: the parse's ds_read2_b32 (8-bit dword offsets) then needs no address add
     uint8_t stage[kStage + 16];  // src[s0 .. s0 + kStage), zero beyond the input
+    uint8_t win[kWinB + 64];     // output [base, base + kWinB) (+ slack for 16-byte reads)
     uint4 desc[kMaxDesc];        // {lit_src, out, lit_len, offset}
 };
 
@@ -296,17 +303,30 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
     const uint32_t lit = tok >> 4, mn = tok & 15u;
     const uint32_t r1 = r + 1u + lit;           // offset bytes (then the ml byte)
     const uint32_t a1 = r1 & ~3u;
+#if APE_LZ4_DREL
+    const l32x2 w = *(const l32x2 *)&L.stage[a1];   // one ds_read_b64 (any byte address)
+    const uint32_t x = funnel(w.y, w.x, r1 & 3u);
+#else
     const uint32_t x = funnel(*(const uint32_t *)&L.stage[a1 + 4], *(const uint32_t *)&L.stage[a1],
                               r1 & 3u);
+#endif
     const uint32_t e = (x >> 16) & 0xFFu;
     z.lit = lit;
     z.off = x & 0xFFFFu;
     z.ipl = P + (int)rel + 1;
     z.ipo = z.ipl + (int)lit + 2;
-    z.fin_in = !FASTD && (uint32_t)z.ipl + lit + 8u > (uint32_t)D.csize;   // ipl >= 1
     const bool mlx = mn == 15u;
     z.mlx = mlx;
+#if APE_LZ4_DREL
+    // on the staged position (s0 + r1 = ipl + lit) against a scalar limit: the same
+    // compares (all values far below 2^31), without the absolute positions
+    const int lim = D.csize - D.s0;   // scalar
+    z.fin_in = !FASTD && (int)r1 > lim - 8;                      // ipl + lit + 8 > csize
+    z.mlerr = !FASTD && mlx && (int)r1 > lim - 2 - kLastLiterals;   // ipo + 5 > csize
+#else
+    z.fin_in = !FASTD && (uint32_t)z.ipl + lit + 8u > (uint32_t)D.csize;   // ipl >= 1
     z.mlerr = !FASTD && mlx && z.ipo + kLastLiterals > D.csize;
+#endif
     z.cx = lit == 15u || (mlx && e == 255u && !z.mlerr);
     z.ml = mlx ? 15u + e : mn;
     z.q = z.ipo + (mlx ? 1 : 0);
@@ -330,14 +350,37 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
     // hop and the J_k hold window positions x 4: ds_bpermute's byte address (it uses
     // address bits [7:2] only), so an exit (>= 64, i.e. >= 256 here) needs no mask
     uint32_t hop;
+#if APE_LZ4_DREL
+    {
+        // the hop alone: mlerr implies fin_in (ipo + 5 = ipl + lit + 7), and the successor
+        // relative to P is lane + lit + 3 (+1 with the ml byte)
+        const Spec z = spec_at<FASTD>(L, D, P, (uint32_t)D.lane);
+        const uint32_t qr = (uint32_t)D.lane + z.lit + (z.mlx ? 4u : 3u);
+        hop = 4u * (z.cx ? kHopCplx : (z.fin_in ? kHopTerm : qr));
+    }
+#else
     {
         const Spec z = spec_at<FASTD>(L, D, P, (uint32_t)D.lane);
         hop = 4u * (z.cx ? kHopCplx : ((z.fin_in || z.mlerr) ? kHopTerm : (uint32_t)(z.q - P)));
     }
+#endif
+#if APE_LZ4_DJMAX
+    // Exits absorb as a max: a real hop moves forward (J[a] > a), and an exit (>= 256) reads
+    // some lane's J through the address wrap but max keeps it >= 256.  A jump from a real
+    // position whose chain reaches its first exit exactly at the jump's end returns that exit
+    // exactly (by induction over k: both halves of J_k are then exact), so lanes up to the
+    // first exit -- the members and the exit X -- are exact; lanes past it hold some value
+    // >= 256 (no member).  One v_max_u32 instead of v_cmp + v_cndmask per jump.
+    auto jump = [](uint32_t J, uint32_t a) {
+        const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)J);
+        return umax(g, a);
+    };
+#else
     auto jump = [](uint32_t J, uint32_t a) {   // exit values absorb
         const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)J);
         return a < 256u ? g : a;
     };
+#endif
     const uint32_t J1 = jump(hop, hop);
     const uint32_t J2 = jump(J1, J1);
     const uint32_t J3 = jump(J2, J2);
