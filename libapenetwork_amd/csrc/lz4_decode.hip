@@ -293,6 +293,10 @@ struct Spec {
     int ipl, ipo, q;                 // first literal byte, after the offset, next token
     bool fin_in, mlerr, cx;          // input ends in the literals / ml bytes run out / complex
     bool mlx;                        // match length nibble 15 (an extension byte follows)
+#if APE_LZ4_DREL
+    bool mlover;                     // ipo + kLastLiterals > csize (mlerr = mlx && mlover)
+    uint32_t r1;                     // staged position after the literals (s0 + r1 = ipl + lit)
+#endif
 };
 
 template <bool FASTD>
@@ -322,7 +326,9 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
     // compares (all values far below 2^31), without the absolute positions
     const int lim = D.csize - D.s0;   // scalar
     z.fin_in = !FASTD && (int)r1 > lim - 8;                      // ipl + lit + 8 > csize
-    z.mlerr = !FASTD && mlx && (int)r1 > lim - 2 - kLastLiterals;   // ipo + 5 > csize
+    z.mlover = (int)r1 > lim - 2 - kLastLiterals;                  // ipo + 5 > csize
+    z.mlerr = !FASTD && mlx && z.mlover;
+    z.r1 = r1;
 #else
     z.fin_in = !FASTD && (uint32_t)z.ipl + lit + 8u > (uint32_t)D.csize;   // ipl >= 1
     z.mlerr = !FASTD && mlx && z.ipo + kLastLiterals > D.csize;
@@ -528,12 +534,23 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
         fm = wave_ballot(fin_in) | wave_ballot((int64_t)cpy > D.oexit);
         badfm = wave_ballot(cpy > ucap) | wave_ballot(iend > (uint32_t)D.csize);
     } else {
+#if APE_LZ4_DREL
+        // cpy + 12 > cap as cpy >= a scalar bound; iend != csize on the staged position
+        const uint32_t capA = ucap > (uint32_t)kMFLimit - 1u ? ucap - ((uint32_t)kMFLimit - 1u) : 0u;
+        fm = wave_ballot(fin_in) | wave_ballot(cpy >= capA);
+        badfm = wave_ballot(z.r1 != (uint32_t)(D.csize - D.s0)) | wave_ballot(cpy > ucap);
+#else
         fm = wave_ballot(fin_in) | wave_ballot(cpy + (uint32_t)kMFLimit > ucap);
         badfm = wave_ballot(iend != (uint32_t)D.csize) | wave_ballot(cpy > ucap);
+#endif
     }
     const bool fin = lane_in(fm);
+#if APE_LZ4_DREL
+    const uint64_t mlm = FASTD ? 0ull : wave_ballot(z.mlx) & wave_ballot(z.mlover);
+#else
     const uint64_t mlm = FASTD ? 0ull
                                : wave_ballot(z.mlx) & wave_ballot(z.ipo + kLastLiterals > D.csize);
+#endif
     const bool e_off = (DICT ? cpy + D.dsz : cpy) < off;               // :1375-1376
     // FASTD: the bytes a sequence needs must lie inside the readable bound (the reference
     // has no bound and reads on; here that is an error, never a read past the buffer)
