@@ -693,8 +693,17 @@ __device__ __forceinline__ void lane_match(WaveLds &L, const Dec &D, uint32_t ba
         if (u1) v1 = lds16(s + t1);
         if (u2) v2 = lds16(s + t2);
         if (u3) v3 = lds16(s + t3);
+    } else if (!DICT) {
+        // dst history (ps >= 0): 32-bit offsets from the scalar base (global_load's SGPR-base
+        // form), no 64-bit address adds
+        gcu8 *d = (gcu8 *)D.dst;
+        const uint32_t o0 = (uint32_t)ps;
+        v0 = gload16_nt(d + o0);
+        if (u1) v1 = gload16_nt(d + (o0 + t1));
+        if (u2) v2 = gload16_nt(d + (o0 + t2));
+        if (u3) v3 = gload16_nt(d + (o0 + t3));
     } else {
-        gcu8 *s = (DICT && ps < 0) ? D.dend + ps : (gcu8 *)D.dst + ps;
+        gcu8 *s = ps < 0 ? D.dend + ps : (gcu8 *)D.dst + ps;
         v0 = gload16_nt(s);
         if (u1) v1 = gload16_nt(s + t1);
         if (u2) v2 = gload16_nt(s + t2);
