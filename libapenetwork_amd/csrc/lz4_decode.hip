@@ -675,10 +675,11 @@ __device__ __forceinline__ void lane_match(WaveLds &L, const Dec &D, uint32_t ba
     // Only the units a lane needs: unit k (k = 1..3) exists when n > 16 k.  Lanes whose
     // match is shorter issue no load for it, so a gather instruction touches only the lines
     // its active lanes need (the texture path's cost is per line: tools/ubench/gather_rate).
-    // The placeholders start at 0, not at v0, so no unit waits for another's load.
+    // The units a lane does not need stay unset (never stored): no v_mov per unit and call,
+    // and no unit waits for another's load.
     const uint32_t t1 = umin(16u, n - 16u), t2 = umin(32u, n - 16u), t3 = n - 16u;
     const bool u1 = n > 16u, u2 = n > 32u, u3 = n > 48u;
-    uint4 v0, v1 = make_uint4(0, 0, 0, 0), v2 = v1, v3 = v1;
+    uint4 v0, v1, v2, v3;
     if (off != 0u && off < n) {   // overlaps itself (off >= 16, n > 16): unit after unit
         const uint8_t *s = L.win + ((uint32_t)ps - base);
         lds_st16(w, lds16(s));
