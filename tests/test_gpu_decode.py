@@ -101,6 +101,84 @@ def _has_off0(c):
     return gen_golden.has_offset0(c)
 
 
+def _dense_block(rng, nseq, p_long_lit, p_long_ml, p_ext):
+    """A valid LZ4 block written token by token (no compressor): mostly 3-6-byte sequences
+    (0-2 literals, a short match), so a 64-byte parse window holds up to 21 members and the
+    lifting's 16-member round and its exits at every lane are exercised; literal lengths >= 15
+    and match lengths with two or more extension bytes (the scalar path) at random places; a
+    16-byte literal tail keeps every match clear of the block-end rules."""
+    out, c = bytearray(), bytearray()
+
+    def ext(v):
+        while v >= 255:
+            c.append(255)
+            v -= 255
+        c.append(v)
+
+    for _ in range(nseq):
+        r = rng.random()
+        lit = rng.randrange(15, 300) if r < p_long_lit else rng.choice((0, 0, 0, 1, 2, 3, 14))
+        if not out and lit == 0:
+            lit = 1
+        r = rng.random()
+        if r < p_long_ml:
+            ml = rng.randrange(19 + 255, 19 + 600)      # two or more extension bytes
+        elif r < p_long_ml + p_ext:
+            ml = rng.randrange(19, 19 + 254)            # one extension byte
+        else:
+            ml = rng.randrange(4, 19)
+        off = rng.randrange(1, min(len(out) + lit, 65535) + 1)
+        c.append((min(lit, 15) << 4) | min(ml - 4, 15))
+        if lit >= 15:
+            ext(lit - 15)
+        lits = bytes(rng.randrange(256) for _ in range(lit))
+        c += lits
+        out += lits
+        c += off.to_bytes(2, "little")
+        if ml - 4 >= 15:
+            ext(ml - 4 - 15)
+        for _ in range(ml):
+            out.append(out[-off])
+    tail = bytes(rng.randrange(256) for _ in range(16))
+    c.append(min(len(tail), 15) << 4)
+    ext(len(tail) - 15)
+    c += tail
+    out += tail
+    return bytes(c), bytes(out)
+
+
+def test_dense_sequences_vs_oracle(cuda, product, oracle):
+    """Hand-built blocks of dense short sequences (up to 21 per 64-byte window), with complex
+    tokens at random positions, then cut short or mutated: return value (including every
+    -(ip)-1) and bytes bit-exact with the oracle, for decompress_safe and _safe_partial."""
+    rng = random.Random(77)
+    comps, caps, tg, whole = [], [], [], []
+    for k in range(240):
+        mix = [(0.0, 0.0, 0.0), (0.02, 0.01, 0.05), (0.1, 0.05, 0.2)][k % 3]
+        c, out = _dense_block(rng, rng.choice((3, 40, 400, 1500)), *mix)
+        c = bytearray(c)
+        if k % 4 == 1:
+            for _ in range(rng.randrange(1, 4)):
+                c[rng.randrange(len(c))] = rng.randrange(256)
+        elif k % 4 == 2:
+            c = c[:rng.randrange(1, len(c) + 1)]
+        comps.append(bytes(c))
+        caps.append(rng.choice((len(out), len(out), len(out) - 1, len(out) + 7)))
+        tg.append(rng.randrange(0, len(out) + 8))
+        whole.append(len(out) if k % 4 in (0, 3) and caps[-1] >= len(out) else None)
+    for targets in (None, tg):
+        rs, outs = run_decode(cuda, product, comps, caps, targets=targets)
+        bad = []
+        for i, (c, cap, r, o) in enumerate(zip(comps, caps, rs, outs)):
+            er, eo = orc_decompress(oracle, c, cap, None if targets is None else targets[i])
+            if r != er or (r > 0 and o != eo[:er] and not _has_off0(c)):
+                bad.append((i, len(c), cap, r, er))
+        assert not bad, bad[:10]
+        if targets is None:   # the generator's blocks are valid: whole ones decode in full
+            assert all(r == n for r, n in zip(rs, whole) if n is not None)
+            assert sum(n is not None for n in whole) >= 60
+
+
 def test_misaligned_buffers(cuda, product, oracle):
     rng = random.Random(5)
     srcs = [I.make(rng.choice(["comp", "text", "rand"]), rng.randrange(1, 65537), seed=i)
