@@ -67,6 +67,9 @@ constexpr uint32_t kLaneMax = 64;  // longest match one lane copies (4 x 16 byte
 #ifndef APE_LZ4_DREL
 #define APE_LZ4_DREL 1             // spec compares on staged positions, one b64 read, hop alone
 #endif
+#ifndef APE_LZ4_DLOOP1
+#define APE_LZ4_DLOOP1 1           // the parse loop with a single exit
+#endif
 #ifndef APE_LZ4_DJMAX
 #define APE_LZ4_DJMAX 1            // lifting jumps absorb exits with a max
 #endif
@@ -1037,6 +1040,18 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
     uint32_t cst = 0;        // output position of desc[0]
     for (;;) {
         // ---- PARSE ----
+#if APE_LZ4_DLOOP1
+        // one exit (a loop with several breaks was structurised into flag phis: s_mov /
+        // s_cselect of 64-bit masks per pass); a complex token may jump far past the staged
+        // bytes, which the loop condition then sees.  (restage may now also hold with nd >= 64:
+        // every descriptor is copied before the restage, as at any restage)
+        while (st == ST_MORE && nd < kBatch && P - D.s0 + kWinNeed <= kStage) {
+            bool cplx;
+            st = parse_window<PARTIAL, DICT, FASTD>(L, D, P, op, nd, result, cplx);
+            if (st == ST_MORE && cplx) st = parse_scalar<PARTIAL, FASTD>(L, D, P, op, nd, result);
+        }
+        const bool restage = st == ST_MORE && P - D.s0 + kWinNeed > kStage;
+#else
         bool restage = false;
         while (st == ST_MORE && nd < kBatch) {
             if (P - D.s0 + kWinNeed > kStage) { restage = true; break; }
@@ -1048,6 +1063,7 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
                 if (st == ST_MORE && P - D.s0 + kWinNeed > kStage) { restage = true; break; }
             }
         }
+#endif
         STAT(0);
         if (st == ST_ERR) break;
         // ---- COPY: batches of <= 64 descriptors; all of them before a restage (their
