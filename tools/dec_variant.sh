@@ -9,7 +9,7 @@ B=libapenetwork_amd/build
 make -s -C libapenetwork_amd/csrc >/dev/null
 mkdir -p $B/decvar_$V
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function \
-    -munsafe-fp-atomics $DEFS -c libapenetwork_amd/csrc/lz4_decode.hip -o $B/decvar_$V/lz4_decode.o
+    -munsafe-fp-atomics -mllvm -amdgpu-sched-strategy=max-ilp $DEFS -c libapenetwork_amd/csrc/lz4_decode.hip -o $B/decvar_$V/lz4_decode.o
 objs=$(ls $B/*.o | grep -v '/lz4_decode.o$')
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o libapenetwork_amd/libape_lz4_amd_$V.so $objs $B/decvar_$V/lz4_decode.o
 echo built libapenetwork_amd/libape_lz4_amd_$V.so

@@ -10,7 +10,8 @@ B=libapenetwork_amd/build
 make -s -C libapenetwork_amd/csrc >/dev/null
 mkdir -p $B/srcvar_$V
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function \
-    -munsafe-fp-atomics -Ilibapenetwork_amd/csrc -Iinclude -c $SRC -o $B/srcvar_$V/$OBJ.o
+    -munsafe-fp-atomics -Ilibapenetwork_amd/csrc -Iinclude $([ "$OBJ" = lz4_decode ] && echo -mllvm -amdgpu-sched-strategy=max-ilp) \
+    -c $SRC -o $B/srcvar_$V/$OBJ.o
 objs=$(ls $B/*.o | grep -v "/$OBJ.o$")
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o libapenetwork_amd/libape_lz4_amd_$V.so $objs $B/srcvar_$V/$OBJ.o
 echo built libapenetwork_amd/libape_lz4_amd_$V.so
