@@ -846,6 +846,21 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
     k1 = umin(k1, (uint32_t)lane - 1u);   // (its own literal is written; lane 0 has no needs)
     const uint64_t need = (lane_in(pm) && lane > 0 && k0 <= k1)
                               ? (((2ull << k1) - 1ull) & ~((1ull << k0) - 1ull)) : 0ull;
+#if defined(APE_LZ4_STATS) && defined(APE_LZ4_STATS_FWD)   // (its atomics distort the timers)
+    {   // diagnostic: pending matches whose sources lie inside one owner's match part (not its
+        // literals), and of those, the ones whose bytes the owner copied from before S0 (one
+        // forwarding step through the owner's offset would make them round-1 ready)
+        const uint32_t mk = bperm(q.m, k0), mek = bperm(q.me, k0), ofk = bperm(q.off, k0);
+        const bool one = lane_in(pm) && lane > 0 && k0 == k1 && x0 >= mk && x1 < mek && ofk != 0u;
+        const bool pre = one && x1 - ofk < mk && x1 - ofk < S0 && x0 >= ofk;
+        const uint64_t onem = wave_ballot(one), prem = wave_ballot(pre);
+        if (lane == 0) {
+            atomicAdd(&g_dec_stats[11], (unsigned long long)__popcll(pm));
+            atomicAdd(&g_dec_stats[12], (unsigned long long)__popcll(onem));
+            atomicAdd(&g_dec_stats[13], (unsigned long long)__popcll(prem));
+        }
+    }
+#endif
     uint64_t done = ~pm;   // lanes still pending = pm & ~done
     wave_sync();
     for (;;) {

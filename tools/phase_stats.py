@@ -14,7 +14,8 @@ os.environ.setdefault("APE_LZ4_LIB", os.path.join(ROOT, "libapenetwork_amd", "li
 sys.path.insert(0, ROOT)
 
 DEC = ["parse", "copy", "(batches)", "(passes after round 1)", "(restages)", "(coop matches)",
-       "(window slides)", "", "", "", "(blocks)", "", "", "", "", ""]
+       "(window slides)", "", "", "", "(blocks)", "(pending matches)", "(in one owner's match)",
+       "(... its bytes from before S0)", "", ""]
 ENC = ["W walk", "W publish", "E write", "W wait end", "W wait mid", "P A+B+C1",
        "P wait mid", "P C2 + S2 + R", "P wait end", "P load waits", "(steps x3 waves)",
        "(members)", "E prepare",
@@ -61,7 +62,8 @@ def main():
                 continue
             per = vals[i] / max(blocks, 1)
             if lab.startswith("("):
-                print("   %-22s %12.1f per block" % (lab, per))
+                if vals[i] or not lab.startswith("(pending") and "owner" not in lab and "S0" not in lab:
+                    print("   %-22s %12.1f per block" % (lab, per))
             else:
                 print("   %-22s %12.0f cyc/block  %5.1f%%" % (lab, per, 100.0 * vals[i] / max(tot, 1)))
     print("verified:", bool((dres == n).all()), "ratio %.4f" % (nb * n / int(csz.sum())))
