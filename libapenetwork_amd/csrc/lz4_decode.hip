@@ -67,6 +67,9 @@ constexpr uint32_t kLaneMax = 64;  // longest match one lane copies (4 x 16 byte
 #ifndef APE_LZ4_DREL
 #define APE_LZ4_DREL 1             // spec compares on staged positions, one b64 read, hop alone
 #endif
+#ifndef APE_LZ4_DFWD
+#define APE_LZ4_DFWD 0             // pending matches forwarded through their owner's offset
+#endif
 #ifndef APE_LZ4_DLOOP1
 #define APE_LZ4_DLOOP1 1           // the parse loop with a single exit
 #endif
@@ -809,8 +812,8 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
     const uint64_t indm = DICT ? wave_ballot(ps + (int)umax(nm, 16u) <= 0) : 0ull;
     const uint64_t lpnm = inwm | ingm | indm;
     const uint64_t lpom = wave_ballot(off >= 16u) & inwm;
-    const uint64_t lpm = wave_ballot(nm >= 4u) & wave_ballot(nm <= kLaneMax) &
-                         (off0m | (ovlm & lpom) | (~ovlm & lpnm));
+    const uint64_t lenm = wave_ballot(nm >= 4u) & wave_ballot(nm <= kLaneMax);
+    const uint64_t lpm = lenm & (off0m | (ovlm & lpom) | (~ovlm & lpnm));
     const bool glb = lane_in(~off0m & ~inwm);
     const int pe = lane_in(off0m) ? -0x7FFFFFFF : (lane_in(ovlm) ? (int)ma : pe0);
     const uint64_t mpm = wave_ballot(nm != 0u);
@@ -828,6 +831,49 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
         else lds_put_small<false>(w, v, nl);
     }
     // round 1
+#if APE_LZ4_DFWD
+    uint64_t r1m = mpm & lpm & wave_ballot(pe <= (int)S0);
+    uint64_t pm = mpm & ~r1m;
+    // sequences owning [max(ps, S0), pe): k0 = owner(first byte), k1 = owner(last byte),
+    // by binary search over the sequence starts (lanes past the batch hold B1)
+    const uint32_t x0 = (uint32_t)(ps > (int)S0 ? ps : (int)S0), x1 = (uint32_t)(pe - 1);
+    uint32_t k0 = 0, k1 = 0;
+    uint32_t offr = off;
+    bool glbr = glb;
+    if (pm) {
+#pragma unroll
+        for (uint32_t st = 32; st >= 1; st >>= 1) {
+            const uint32_t c0 = k0 + st, c1 = k1 + st;
+            const uint32_t v0 = bperm(q.o, c0), v1 = bperm(q.o, c1);
+            k0 = v0 <= x0 ? c0 : k0;
+            k1 = v1 <= x1 ? c1 : k1;
+        }
+        // Forwarding: a pending match whose sources [ps, pe) lie inside the match of one
+        // earlier sequence k, which copied them from [ps - off_k, pe - off_k), bytes before
+        // that match and before S0 (final: window, dst history or dictionary), reads those
+        // bytes in round 1 -- at offset off + off_k (no self-overlap then: the new sources
+        // end before ma).  ~40 % of the pending matches on App. C data
+        // (profiles/r4_dec_forwarding_counts.txt).
+        const uint32_t mk = bperm(q.m, k0), mek = bperm(q.me, k0), ofk = bperm(q.off, k0);
+        const int psf = ps - (int)ofk, pef = pe0 - (int)ofk;
+        const uint64_t inwf = wave_ballot(psf >= (int)base);
+        uint64_t ingf = wave_ballot(pef <= (int)W.gdone) &
+                        (wave_ballot(nm >= 16u) | wave_ballot(psf + 16 <= D.cap));
+        if (DICT) ingf &= wave_ballot(psf >= 0);
+        const uint64_t indf = DICT ? wave_ballot(psf + (int)umax(nm, 16u) <= 0) : 0ull;
+        const uint64_t fwm = pm & lenm & ~off0m & ~ovlm & wave_ballot(k0 == k1) &
+                             wave_ballot(k0 < (uint32_t)lane) & wave_ballot(ofk != 0u) &
+                             wave_ballot(ps >= (int)mk) & wave_ballot(pe0 <= (int)mek) &
+                             wave_ballot(pef <= (int)mk) & wave_ballot(pef <= (int)S0) &
+                             (inwf | ingf | indf);
+        offr = lane_in(fwm) ? off + ofk : off;
+        glbr = lane_in((fwm & ~inwf) | (~fwm & ~off0m & ~inwm));
+        r1m |= fwm;
+        pm &= ~fwm;
+    }
+    lane_match<DICT>(L, D, base, lane_in(r1m), ma, nm, offr, glbr);
+    if (!pm) return;
+#else
     const uint64_t r1m = mpm & lpm & wave_ballot(pe <= (int)S0);
     lane_match<DICT>(L, D, base, lane_in(r1m), ma, nm, off, glb);
     uint64_t pm = mpm & ~r1m;
@@ -843,6 +889,7 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
         k0 = v0 <= x0 ? c0 : k0;
         k1 = v1 <= x1 ? c1 : k1;
     }
+#endif
     k1 = umin(k1, (uint32_t)lane - 1u);   // (its own literal is written; lane 0 has no needs)
     const uint64_t need = (lane_in(pm) && lane > 0 && k0 <= k1)
                               ? (((2ull << k1) - 1ull) & ~((1ull << k0) - 1ull)) : 0ull;
