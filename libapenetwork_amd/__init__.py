@@ -415,9 +415,20 @@ class Chain:
             raise ValueError("need %d fds" % self.nconn)
         return (_C.c_int * self.nconn)(*fds)
 
+    def _rows(self, a, what):
+        """The C side takes one stride: row pitch = nconn x strides[1], >= msg_len contiguous
+        bytes per row."""
+        import numpy as np
+        if (not isinstance(a, np.ndarray) or a.dtype != np.uint8 or a.ndim != 3
+                or a.shape[1] != self.nconn or a.shape[2] < self.msg_len or a.strides[2] != 1
+                or a.strides[1] < self.msg_len or a.strides[0] != self.nconn * a.strides[1]):
+            raise ValueError("%s: need a uint8 array [nmsg, %d, >= %d] with contiguous rows"
+                             % (what, self.nconn, self.msg_len))
+
     def send(self, fds, msgs):
         """msgs: uint8 numpy [nmsg, nconn, S >= msg_len] (round m, connection i).  Returns the
         bytes written."""
+        self._rows(msgs, "msgs")
         nmsg = int(msgs.shape[0])
         r = lib().APE_LZ4_chain_send(self._c, self._fds(fds), _C.c_void_p(msgs.ctypes.data),
                                      int(msgs.strides[1]), nmsg)
@@ -428,6 +439,11 @@ class Chain:
     def recv(self, fds, out, status):
         """out: uint8 numpy [nmsg, nconn, S >= msg_len]; status: int32 numpy [nconn].  Returns
         the payload bytes (raises on a malformed stream or a failed decode)."""
+        import numpy as np
+        self._rows(out, "out")
+        if (not isinstance(status, np.ndarray) or status.dtype != np.int32
+                or status.shape != (self.nconn,) or not status.flags["C_CONTIGUOUS"]):
+            raise ValueError("status: need a contiguous int32 array [%d]" % self.nconn)
         nmsg = int(out.shape[0])
         r = lib().APE_LZ4_chain_recv(self._c, self._fds(fds), _C.c_void_p(out.ctypes.data),
                                      int(out.strides[1]), nmsg, _C.c_void_p(status.ctypes.data))

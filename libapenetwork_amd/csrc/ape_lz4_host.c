@@ -352,6 +352,12 @@ int decode_core(const byte *src, byte *dst, int isize, int osize, int safe, int 
         const byte *ref;
         if (len == 15) {
             unsigned s;
+            /* The reference reads the first length byte unconditionally (ref :1330-1337), one
+             * byte past src when the token is the last input byte.  That byte cannot change
+             * the outcome: with ip past iend every later check fails and the result is
+             * -(consumed + 1) - 1 whatever it holds, so return that without reading it.  Only
+             * the first read can be out of range: the loop condition bounds the others. */
+            if (safe && ip >= iend) return -(int)(ip - src) - 2;
             do {
                 s = *ip++;
                 len += s;

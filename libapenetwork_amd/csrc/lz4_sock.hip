@@ -563,6 +563,10 @@ struct ChainPart {
     long long *h_poff[2] = {nullptr, nullptr};
     int *h_csz[2] = {nullptr, nullptr}, *h_res[2] = {nullptr, nullptr};
     uint32_t rxpos = 0;
+    // per-connection receive buffers, kept across recv calls: a read may take in frames beyond
+    // the messages one call needs, and the next call on the chain resumes with those bytes
+    std::vector<APE_LZ4_rxbuf *> rb;
+    std::vector<char> eof;
 };
 
 namespace {
@@ -583,6 +587,7 @@ void chain_release(ChainPart *c) {
                     (void *)c->h_poff[1], (void *)c->h_csz[0], (void *)c->h_csz[1],
                     (void *)c->h_res[0], (void *)c->h_res[1]})
         if (p) (void)hipHostFree(p);
+    for (APE_LZ4_rxbuf *b : c->rb) APE_LZ4_rxbuf_free(b);
     for (hipEvent_t e : {c->tev[0], c->tev[1], c->rev[0], c->rev[1]})
         if (e) (void)hipEventDestroy(e);
     if (c->tst) (void)hipStreamDestroy(c->tst);
@@ -702,9 +707,12 @@ long long part_send(ChainPart *c, const int *fds, const char *h_msgs, size_t msg
         long long t0 = now_ns();
         if (hipEventSynchronize(c->tev[b]) != hipSuccess) { rc = APE_LZ4_GPU_ELAUNCH; break; }
         const long long *off = c->h_off[b];
-        const long long tot = off[nt];
-        // a chunk that did not fit its bound is a codec failure (never for valid sizes)
-        if (tot <= 4ll * nt) { rc = APE_LZ4_GPU_ELAUNCH; break; }
+        // a chunk that did not fit its bound is a codec failure (never for valid sizes): its
+        // csz <= 0 would go out as a frame the reference receiver rejects, so any one fails
+        // the round (frame j spans off[j+1] - off[j] = 4 + csz bytes)
+        for (int j = 0; j < nt && rc == 0; j++)
+            if (off[j + 1] - off[j] <= 4) rc = APE_LZ4_GPU_ELAUNCH;
+        if (rc) break;
         sock_add(4, now_ns() - t0);
         sock_add(5, 1);
         if (r + 1 < nr) rc = launch(r + 1);   // the next round's GPU work under these writes
@@ -733,17 +741,23 @@ long long part_recv(ChainPart *c, const int *fds, char *h_out, size_t out_stride
     if (hipSetDevice(c->dev) != hipSuccess) return APE_LZ4_GPU_ENODEV;
     const int M = c->nconn, nch = c->nch, nr = (nmsg + c->K - 1) / c->K;
     const int maxf = c->K * nch;   // frames of a full round per connection
-    std::vector<APE_LZ4_rxbuf *> rb((size_t)M, nullptr);
     std::vector<long long> offs((size_t)M * (maxf + 1), 0);
     std::vector<int> parsed((size_t)M, 0);
-    std::vector<char> eof((size_t)M, 0);
     std::vector<pollfd> pf((size_t)M);
     std::vector<int> pmap((size_t)M);
     int rc = 0;
+    if (c->rb.empty()) {
+        c->rb.assign((size_t)M, nullptr);
+        c->eof.assign((size_t)M, 0);
+    }
+    std::vector<APE_LZ4_rxbuf *> &rb = c->rb;
+    std::vector<char> &eof = c->eof;
     for (int i = 0; i < M; i++) {   // host-only buffers: the payloads go to the GPU through
         h_status[i] = 0;            // the pinned staging area, so no per-connection registration
-        rb[i] = (APE_LZ4_rxbuf *)calloc(1, sizeof(APE_LZ4_rxbuf));
-        if (rb[i]) rb[i]->registered = -1;
+        if (!rb[i]) {
+            rb[i] = (APE_LZ4_rxbuf *)calloc(1, sizeof(APE_LZ4_rxbuf));
+            if (rb[i]) rb[i]->registered = -1;
+        }
         if (!rb[i] || APE_LZ4_rxbuf_prepare(rb[i], 1u << 16) != 0) rc = APE_LZ4_GPU_ENOMEM;
     }
     auto round_k = [&](int r) { return nmsg - r * c->K < c->K ? nmsg - r * c->K : c->K; };
@@ -899,8 +913,10 @@ long long part_recv(ChainPart *c, const int *fds, char *h_out, size_t out_stride
         const int r2 = check(b);
         if (rc == 0) rc = r2;
     }
+    // an error path may leave copies into h_out / out of h_stage queued for a round that never
+    // became busy: nothing of this call is in flight when it returns
+    if (hipStreamSynchronize(c->rst) != hipSuccess && rc == 0) rc = APE_LZ4_GPU_ELAUNCH;
     sock_add(7, now_ns() - t_all);
-    for (int i = 0; i < M; i++) APE_LZ4_rxbuf_free(rb[i]);
     return rc ? rc : got;
 }
 

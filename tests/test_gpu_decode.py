@@ -407,3 +407,33 @@ def test_benchmark_blocks_vs_reference_itself(cuda, product, cfg):
             assert r == er, (b, cap, r, er)
             if er > 0:
                 assert out == o.raw[:er] == host[b].tobytes()[:er], (b, cap)
+
+
+def test_final_token_literal_run_ignores_bytes_past_src(cuda, product, oracle):
+    """a token with literal length 15 as the last input byte (`[0xFF]`, csize 1).
+    The reference reads one byte past src there (ref src/ape_lz4.c:1330-1337) and returns
+    -(csize + 1) - 1 whatever it holds; the GPU decoder's staging masks everything beyond
+    csize, so the byte that follows in memory (varied here) cannot matter either.  (Only a
+    first token can be the last byte: after a sequence the safe checks leave >= 4 bytes.)"""
+    cases = []
+    for blob in (b"\xff", b"\xf0", b"\xf7", b"\x10a\xf0", b"\x10a\xff"):
+        for after in (b"\x00", b"\xff", b"\x05" * 40):
+            for cap in (1, 64, 4096):
+                cases.append((blob, after, cap))
+    stored = [b + a for b, a, _ in cases]
+    ins, iptr, _ = pack(cuda, stored)
+    sizes = ints(cuda, [len(b) for b, _, _ in cases])
+    caps = [c for _, _, c in cases]
+    for partial in (False, True):
+        dst, dptr, _ = alloc_out(cuda, caps)
+        res = ints(cuda, [0] * len(cases))
+        if partial:
+            product.decompress_partial_batch(iptr, sizes, dptr, ints(cuda, [10] * len(cases)),
+                                             ints(cuda, caps), res)
+        else:
+            product.decompress_ptr_batch(iptr, sizes, dptr, ints(cuda, caps), res)
+        cuda.cuda.synchronize()
+        got = res.cpu().tolist()
+        exp = [orc_decompress(oracle, b, cap, 10 if partial else None)[0] for b, _, cap in cases]
+        assert got == exp, [(c[0], c[2], g, e) for c, g, e in zip(cases, got, exp) if g != e]
+        assert all(g == -3 for (b, _, _), g in zip(cases, got) if len(b) == 1), got

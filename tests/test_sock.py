@@ -443,6 +443,64 @@ def test_chain_reference_tx_decoded_by_gpu(cuda, product, monkeypatch, msg_len, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("split,per_round", [((2, 1, 4), 2), ((1, 6), 0), ((3, 3, 1), 16)])
+def test_chain_recv_resumes_across_calls(cuda, product, monkeypatch, split, per_round):
+    """the sender writes all messages at once, so one read can take in frames past
+    the messages a recv call needs; those bytes stay with the chain and the next recv on it
+    resumes mid-stream against the right 64 KiB history.  Several recv calls, every byte
+    compared."""
+    if per_round:
+        monkeypatch.setenv("APE_LZ4_CHAIN_ROUND", str(per_round))
+    nconn, msg_len, nmsg = 3, 65536, sum(split)
+    peer = _ref_peer()
+    msgs = _chain_msgs(cuda, product, nmsg, nconn, msg_len, seed=99)
+    streams = [_ref_tx(peer, [msgs[m, i].tobytes() for m in range(nmsg)]) for i in range(nconn)]
+    pairs = [_pair() for _ in range(nconn)]
+
+    def txf(i):
+        pairs[i][0].sendall(streams[i])
+        pairs[i][0].shutdown(socket.SHUT_WR)
+
+    ths = [threading.Thread(target=txf, args=(i,)) for i in range(nconn)]
+    for t in ths:
+        t.start()
+    ch = product.Chain(nconn, msg_len)
+    m0 = 0
+    for k in split:
+        out = np.full((k, nconn, msg_len), 0xCB, dtype=np.uint8)
+        status = np.full(nconn, -9, dtype=np.int32)
+        got = ch.recv([r.fileno() for _, r in pairs], out, status)
+        assert got == k * nconn * msg_len and (status == 0).all(), (m0, status)
+        assert np.array_equal(out, msgs[m0:m0 + k]), m0
+        m0 += k
+    ch.free()
+    for t in ths:
+        t.join()
+    for t, r in pairs:
+        t.close()
+        r.close()
+
+
+def test_chain_argument_checks(product):
+    """Chain.send/recv check the array shapes, dtypes and strides the C side
+    assumes (one row pitch = nconn x strides[1]; int32 status of length nconn)."""
+    ch = object.__new__(product.Chain)
+    ch.nconn, ch.msg_len, ch._c = 4, 100, None
+    ok = np.zeros((2, 4, 100), dtype=np.uint8)
+    ch._rows(ok, "msgs")
+    ch._rows(np.zeros((2, 4, 128), dtype=np.uint8), "msgs")
+    for bad in (np.zeros((2, 4, 99), dtype=np.uint8), np.zeros((2, 3, 100), dtype=np.uint8),
+                np.zeros((2, 4, 100), dtype=np.int8), np.zeros((2, 4, 200), dtype=np.uint8)[:, :, ::2],
+                np.zeros((4, 2, 100), dtype=np.uint8).transpose(1, 0, 2), np.zeros((4, 100), dtype=np.uint8)):
+        with pytest.raises(ValueError):
+            ch._rows(bad, "msgs")
+    with pytest.raises(ValueError):
+        ch.recv([0, 1, 2, 3], ok, np.zeros(4, dtype=np.int64))
+    with pytest.raises(ValueError):
+        ch.recv([0, 1, 2, 3], ok, np.zeros(3, dtype=np.int32))
+
+
+@pytest.mark.gpu
 def test_chain_gpu_roundtrip_and_malformed(cuda, product):
     """GPU TX -> loopback -> GPU RX over 8 connections, every byte compared; then a stream
     with one mutated block fails that connection (status != 0, GpuError), and a truncated one
