@@ -1551,8 +1551,19 @@ lz4_encode_kernel(BlockArgs a) {
     else encode_block<false, ACC>(S, B, wave, lane, &a.result[b]);
 }
 
+// compress_default (acceleration 1, no prefix) runs the segment-parallel encoder
+// (lz4_encode_seg.hip) when APE_LZ4_ENCODER=seg selects it (A/B until measured)
+static bool use_seg_encoder() {
+    static const int v = [] {
+        const char *e = getenv("APE_LZ4_ENCODER");
+        return (e && e[0] == 's') ? 1 : 0;
+    }();
+    return v != 0;
+}
+
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
+    if (a.accel <= 1 && !a.dict_size && use_seg_encoder()) return launch_encode_seg(a, s);
     if (a.accel > 1)
         hipLaunchKernelGGL(lz4_encode_kernel<true>, dim3(a.nblocks), dim3(192), 0, s, a);
     else

@@ -1,0 +1,475 @@
+// lz4_encode_seg.hip -- MI355X (gfx950) batched LZ4 block encoder, segment-parallel form.
+//
+// Replaces the per-block work of APE_LZ4_compress_default (ref src/ape_lz4.c:811-815 ->
+// LZ4_compress_generic :530-755, byU16 / noDict, acceleration 1).  Like the reference it is
+// a greedy LZ77 parse over a hash of 5 bytes; unlike it, the parse of one 64 KiB block is
+// cut into 1024 independent 64-byte segments that 1024 lanes parse at once, against an
+// index of the whole block that is built before any parsing.  The output is a valid LZ4
+// v1.7.1 block (every rule decompress_safe enforces, :1346-1366, :1375, :1444-1447: matches
+// start at <= n-12 and end at <= n-5, the last >= 5 bytes are literals), decoded by the
+// reference itself in the tests; the bytes differ from the reference's.
+//
+// One 1024-thread workgroup (16 waves) per block, the whole block in LDS (64 KiB) next to
+// its index, so that no parse step touches global memory:
+//
+//   LOAD   the block into LDS with 16-byte coalesced loads (its 16-byte-aligned chunks).
+//   INDEX  every 4th position p (p <= n-13) hashed (5 bytes, 10 bits) and bucket-sorted by
+//          a stable counting sort: per-wave bucket counts (wave w holds positions
+//          [4096w, 4096w+4096)), a block-wide scan, then each wave scatters its own
+//          positions in order -> pos[] holds each bucket's positions in ascending order.
+//          Deterministic: no two waves ever update the same counter.
+//   PARSE  lane k parses segment [64k, 64k+64) greedily, as the reference's search loop
+//          (:591-619): at position q the bucket of hash(q) is binary-searched for the
+//          four latest indexed positions < q; each is measured against q over 16 bytes
+//          (LDS reads + v_alignbyte, xor, v_ffbl) and the longest wins (ties: the most
+//          recent); a 16-byte match is extended 16 bytes at a time; catch-up backwards
+//          into the segment's pending literals (:623-627).  A match may run up to 64
+//          bytes past the segment end.  Records {start, length, offset} go to LDS.
+//   SPLICE the end of each segment's last match, prefix-maxed over segments, is where the
+//          next segment's kept sequences start: matches inside it are dropped, one that
+//          straddles it is cut (kept if >= 4 bytes); literal runs join across segments.
+//          Per-segment output sizes are prefix-summed into output offsets.
+//   EMIT   each lane writes its sequences (token, length bytes, literals, offset) into an
+//          LDS staging window (runs longer than 64 literals are copied by the whole wave),
+//          and the window is stored to dst with coalesced stores; >36 KiB outputs take
+//          more than one window.  A block the parse cannot shrink is stored as one literal
+//          run, as the reference stores incompressible input (:732-751).
+//
+// Searching the latest four candidates instead of one gives a better ratio than the
+// reference's single-candidate table (tools/seg_model.c: 3.30 vs 3.157 on SURVEY App. C
+// data); the index of every 4th position and the segment cut cost little (catch-up finds
+// the true match start; a segment's last match may overrun into the next segment).
+#include "lz4_gpu_internal.h"
+
+namespace apelz4 {
+
+namespace {
+
+constexpr int kSThreads = 1024, kSWaves = kSThreads / 64;
+constexpr int kSSeg = kMaxBlock / kSThreads;     // 64 bytes per segment (lane)
+constexpr int kSStride = 4;                       // indexed positions: multiples of 4
+constexpr int kSHLog = 10, kSBuckets = 1 << kSHLog;
+constexpr int kSIdx = kMaxBlock / kSStride;       // 16384 index entries
+constexpr int kSCapX = 64;                        // a match may end this far past its segment
+constexpr int kSRec = 14;                         // record slots per segment
+constexpr int kSDepth = 4;                        // candidates measured per position
+constexpr int kSLongRun = 64;                     // longer literal runs: copied by the wave
+constexpr int kSBlkW = (kMaxBlock + 64) / 4;      // block bytes at offset a (< 16) + padding
+
+struct SegLds {
+    uint32_t blk[kSBlkW];
+    union {
+        struct {
+            uint16_t pos[kSIdx];
+            uint32_t offs[kSBuckets + 1];
+        } ix;
+        uint8_t stage[kSIdx * 2 + (kSBuckets + 1) * 4];
+    } u;
+    union {
+        uint32_t cnt[kSWaves * kSBuckets / 2];    // index build: per-wave u16 counters, packed
+        uint32_t rec[kSRec * kSThreads];          // parse: record r of lane k at [r*1024 + k]
+    } r;
+    uint32_t wsum[kSWaves];
+    uint32_t wmax[kSWaves];
+};
+constexpr int kSStage = (int)sizeof(((SegLds *)0)->u.stage) & ~15;
+static_assert(sizeof(SegLds) <= 160 * 1024, "LDS");
+static_assert(kSSeg == 64, "segment = 64 bytes (record start field: 6 bits)");
+
+__device__ __forceinline__ uint32_t sffbl(uint32_t d) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(d));
+    return r;
+}
+
+// hash of the 5 bytes x (little-endian dword) + b4 onto kSHLog bits: two full-rate 24-bit
+// multiplies (v_mul_u32_u24 / v_mad_u32_u24)
+__device__ __forceinline__ uint32_t shash(uint32_t x, uint32_t b4) {
+    const uint32_t lo = x & 0xFFFFFFu, hi = (x >> 24) | ((b4 & 0xFFu) << 8);
+    return (__umul24(lo, 0x9E3779u) + __umul24(hi, 0xC2B2AEu)) >> (32 - kSHLog);
+}
+
+// 16 bytes at byte address x of the block buffer: aligned dword reads + v_alignbyte
+__device__ __forceinline__ uint4 lds16(const SegLds &S, uint32_t x) {
+    const uint32_t *r = S.blk + (x >> 2);
+    const uint32_t sh = x & 3u;
+    const uint32_t w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3], w4 = r[4];
+    return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                      __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+}
+__device__ __forceinline__ uint32_t lds4(const SegLds &S, uint32_t x) {
+    const uint32_t *r = S.blk + (x >> 2);
+    return __builtin_amdgcn_alignbyte(r[1], r[0], x & 3u);
+}
+__device__ __forceinline__ uint32_t ldsb(const SegLds &S, uint32_t x) {
+    return ((const uint8_t *)S.blk)[x];
+}
+
+// common prefix of A and B in bytes (0..16): first differing bit by ffbl + saturating add + min
+__device__ __forceinline__ uint32_t prefix16(uint4 A, uint4 B) {
+    uint32_t m = sffbl(A.x ^ B.x);
+    m = umin(m, __builtin_elementwise_add_sat(sffbl(A.y ^ B.y), 32u));
+    m = umin(m, __builtin_elementwise_add_sat(sffbl(A.z ^ B.z), 64u));
+    m = umin(m, __builtin_elementwise_add_sat(sffbl(A.w ^ B.w), 96u));
+    return umin(m, 128u) >> 3;
+}
+
+__device__ __forceinline__ int extlen(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
+
+// block-wide exclusive sum over the 1024 threads; *total = the sum of all
+__device__ __forceinline__ uint32_t block_excl_sum(SegLds &S, uint32_t v, int wave, int lane,
+                                                   uint32_t *total) {
+    const uint32_t inc = wave_incl_sum(v);
+    if (lane == 63) S.wsum[wave] = inc;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kSWaves; w++) {
+        const uint32_t t = S.wsum[w];
+        before += w < wave ? t : 0u;
+        all += t;
+    }
+    __syncthreads();
+    *total = all;
+    return before + inc - v;
+}
+
+// block-wide exclusive max (0 for thread 0); *total = the max of all
+__device__ __forceinline__ uint32_t block_excl_max(SegLds &S, uint32_t v, int wave, int lane,
+                                                   uint32_t *total) {
+    const uint32_t inc = wave_incl_max(v);
+    if (lane == 63) S.wmax[wave] = inc;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kSWaves; w++) {
+        const uint32_t t = S.wmax[w];
+        before = w < wave ? umax(before, t) : before;
+        all = umax(all, t);
+    }
+    __syncthreads();
+    *total = all;
+    return umax(before, wave_shr1(inc, 0u));
+}
+
+// one output byte at absolute position o, if it falls into the staging window [w0, w0+kSStage)
+__device__ __forceinline__ void put(SegLds &S, uint32_t o, uint32_t w0, uint32_t v) {
+    const uint32_t i = o - w0;
+    if (i < (uint32_t)kSStage) S.u.stage[i] = (uint8_t)v;
+}
+
+// the length bytes after a token nibble of 15: (v - 15) / 255 bytes of 255 and the rest
+__device__ __forceinline__ uint32_t put_len(SegLds &S, uint32_t o, uint32_t w0, int v) {
+    v -= 15;
+    for (; v >= 255; v -= 255) put(S, o++, w0, 255u);
+    put(S, o++, w0, (uint32_t)v);
+    return o;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) {
+    __shared__ SegLds S;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const char *srcp = a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride;
+    char *dstp = a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride;
+    const int n = a.src_size[b];
+    const int cap = a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride;
+    if (n < 0 || n > kMaxBlock || cap < 0) {
+        if (tid == 0) a.result[b] = (n > kMaxBlock) ? kErange : 0;
+        return;
+    }
+
+    // ---- LOAD: the 16-byte-aligned chunks that hold the block's bytes; byte i of the
+    // block lands at blk byte a0 + i.  Chunks outside the block are never read (a chunk
+    // with one valid byte lies in the same page as that byte); the padding is zeroed.
+    const uint32_t a0 = (uint32_t)((uintptr_t)srcp & 15u);
+    {
+        const u32x4_u *g = (const u32x4_u *)(srcp - a0);
+        const int nch = n > 0 ? (int)((a0 + (uint32_t)n + 15u) >> 4) : 0;
+        uint4 *L = (uint4 *)S.blk;
+        for (int c = tid; c < kSBlkW / 4; c += kSThreads) {
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (c < nch) {
+                const u32x4_u t = __builtin_nontemporal_load(g + c);
+                v = make_uint4(t.x, t.y, t.z, t.w);
+            }
+            L[c] = v;
+        }
+        for (int i = tid; i < kSWaves * kSBuckets / 2; i += kSThreads) S.r.cnt[i] = 0u;
+    }
+    __syncthreads();
+
+    // ---- INDEX: stable counting sort of positions 4i (4i <= n-13) by hash ----
+    const int nidx = n >= 13 ? (n - 13) / kSStride + 1 : 0;
+    uint32_t hv[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int i = wave * 1024 + r * 64 + lane;
+        hv[r] = kSBuckets;
+        if (i < nidx) {
+            const uint32_t x = a0 + (uint32_t)(i * kSStride);
+            hv[r] = shash(lds4(S, x), ldsb(S, x + 4));
+            atomicAdd(&S.r.cnt[wave * (kSBuckets / 2) + (hv[r] >> 1)], (hv[r] & 1u) ? 0x10000u : 1u);
+        }
+    }
+    __syncthreads();
+    {
+        const int h = tid;   // one bucket per thread
+        uint32_t start[kSWaves], run = 0;
+#pragma unroll
+        for (int w = 0; w < kSWaves; w++) {
+            const uint32_t c = (S.r.cnt[w * (kSBuckets / 2) + (h >> 1)] >> ((h & 1) * 16)) & 0xFFFFu;
+            start[w] = run;
+            run += c;
+        }
+        uint32_t tot;
+        const uint32_t base = block_excl_sum(S, run, wave, lane, &tot);
+        S.u.ix.offs[h] = base;
+        if (h == kSBuckets - 1) S.u.ix.offs[kSBuckets] = tot;
+        uint16_t *c16 = (uint16_t *)S.r.cnt;
+#pragma unroll
+        for (int w = 0; w < kSWaves; w++) c16[w * kSBuckets + h] = (uint16_t)(base + start[w]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; r++) {   // in order: a wave's positions enter each bucket ascending
+        if (hv[r] < (uint32_t)kSBuckets) {
+            const uint32_t old = atomicAdd(&S.r.cnt[wave * (kSBuckets / 2) + (hv[r] >> 1)],
+                                           (hv[r] & 1u) ? 0x10000u : 1u);
+            const uint32_t slot = (old >> ((hv[r] & 1u) * 16)) & 0xFFFFu;
+            S.u.ix.pos[slot] = (uint16_t)((wave * 1024 + r * 64 + lane) * kSStride);
+        }
+    }
+    __syncthreads();
+
+    // ---- PARSE: lane tid, segment [s0, s1) ----
+    const int s0 = tid * kSSeg;
+    const int mfl = n - 12;                  // matches start at <= n-12 (:585)
+    int nrec = 0;
+    if (s0 < n) {
+        const int s1 = s0 + kSSeg < n ? s0 + kSSeg : n;
+        // matches end at <= n-12 (not n-5): a match cut to start where the previous
+        // segment's coverage ends then still starts at <= n-12
+        const int capE = s1 + kSCapX < mfl ? s1 + kSCapX : mfl;
+        int q = s0 > 1 ? s0 : 1, anchor = s0;
+        while (q < s1 && q <= mfl && nrec < kSRec) {
+            const uint4 own = lds16(S, a0 + (uint32_t)q);
+            const uint32_t h = shash(own.x, own.y);
+            int lo = (int)S.u.ix.offs[h], hi = (int)S.u.ix.offs[h + 1];
+            const int blo = lo;
+            while (lo < hi) {   // first entry >= q
+                const int mid = (lo + hi) >> 1;
+                if ((int)S.u.ix.pos[mid] < q) lo = mid + 1;
+                else hi = mid;
+            }
+            const int room = capE - q;
+            int best = 0, bestc = 0;
+#pragma unroll
+            for (int d = 0; d < kSDepth; d++) {
+                const int j = lo - 1 - d;
+                if (j >= blo) {
+                    const int c = (int)S.u.ix.pos[j];
+                    int l = (int)prefix16(own, lds16(S, a0 + (uint32_t)c));
+                    l = l < room ? l : room;
+                    if (l > best) { best = l; bestc = c; }
+                }
+            }
+            if (best < kMinMatch) { q++; continue; }
+            int len = best;
+            if (best == 16) {
+                while (len < room) {
+                    const int l = (int)prefix16(lds16(S, a0 + (uint32_t)(q + len)),
+                                                lds16(S, a0 + (uint32_t)(bestc + len)));
+                    len += l;
+                    if (l < 16) break;
+                }
+                len = len < room ? len : room;
+            }
+            int m = q, c = bestc;   // catch-up (:623-627)
+            while (m > anchor && c > 0 && ldsb(S, a0 + (uint32_t)(m - 1)) == ldsb(S, a0 + (uint32_t)(c - 1))) {
+                m--;
+                c--;
+                len++;
+            }
+            S.r.rec[nrec * kSThreads + tid] = (uint32_t)(m - s0) | ((uint32_t)len << 6) | ((uint32_t)(m - c) << 16);
+            nrec++;
+            anchor = m + len;
+            q = anchor;
+        }
+    }
+
+    // ---- SPLICE: where each segment's kept sequences start; sizes; output offsets ----
+    // Coverage after segment k: C_k = f_k(C_{k-1}), f_k(c) = c + 4 <= e_k ? e_k : c with e_k
+    // the end of k's last match (a match cut to start at c is kept only if >= 4 bytes; all
+    // of k's earlier matches end before its last one starts).  C is the fixed point of
+    // cover = exclusive-prefix-max(f(cover)), reached from the plain prefix max of e in one
+    // or two rounds (a cut < 4 bytes is rare); a sequential pass settles the rest.
+    uint32_t elast = 0;
+    if (nrec > 0) {
+        const uint32_t r = S.r.rec[(nrec - 1) * kSThreads + tid];
+        elast = (uint32_t)s0 + (r & 63u) + ((r >> 6) & 1023u);
+    }
+    uint32_t cover_all;
+    uint32_t cover = block_excl_max(S, elast, wave, lane, &cover_all);
+    for (int it = 0;; it++) {
+        const uint32_t E = cover + 4u <= elast ? elast : cover;
+        uint32_t all2;
+        const uint32_t c2 = block_excl_max(S, E, wave, lane, &all2);
+        const bool moved = c2 != cover;
+        cover = c2;
+        cover_all = all2;
+        if (!__syncthreads_or(moved)) break;
+        if (it == 3) {   // sequential: thread 0 walks the segments (ends in LDS)
+            uint32_t *ends = (uint32_t *)S.u.stage;
+            ends[tid] = elast;
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t c = 0;
+                for (int k = 0; k < kSThreads; k++) {
+                    const uint32_t e = ends[k];
+                    ends[k] = c;
+                    if (c + 4u <= e) c = e;
+                }
+                S.wmax[0] = c;
+            }
+            __syncthreads();
+            cover = ends[tid];
+            cover_all = S.wmax[0];
+            __syncthreads();
+            break;
+        }
+    }
+    uint32_t sz = 0;
+    {
+        uint32_t pe = cover;
+        for (int r = 0; r < nrec; r++) {
+            const uint32_t w = S.r.rec[r * kSThreads + tid];
+            uint32_t m = (uint32_t)s0 + (w & 63u), len = (w >> 6) & 1023u;
+            const uint32_t e = m + len;
+            if (e <= pe) continue;
+            if (m < pe) {
+                len = e - pe;
+                m = pe;
+                if (len < (uint32_t)kMinMatch) continue;
+            }
+            const int lit = (int)(m - pe);
+            sz += 1u + (uint32_t)extlen(lit) + (uint32_t)lit + 2u + (uint32_t)extlen((int)len - 4);
+            pe = e;
+        }
+    }
+    uint32_t body;
+    const uint32_t obase = block_excl_sum(S, sz, wave, lane, &body);
+    const int lastrun = n - (int)cover_all;
+    const uint32_t total = body + 1u + (uint32_t)extlen(lastrun) + (uint32_t)lastrun;
+    const uint32_t litonly = 1u + (uint32_t)extlen(n) + (uint32_t)n;
+
+    if (total >= litonly) {
+        // ---- incompressible: one literal run (what the reference emits for such input) ----
+        if (litonly > (uint32_t)cap) {
+            if (tid == 0) a.result[b] = 0;
+            return;
+        }
+        const int hdr = 1 + extlen(n);
+        uint8_t *d = (uint8_t *)dstp;
+        for (int i = tid; i < hdr; i += kSThreads)
+            d[i] = (uint8_t)(i == 0 ? (n >= 15 ? 0xF0 : n << 4) : (i < hdr - 1 ? 255 : (n - 15) % 255));
+        for (int i = tid; i < n; i += kSThreads) d[hdr + i] = (uint8_t)ldsb(S, a0 + (uint32_t)i);
+        if (tid == 0) a.result[b] = (int)litonly;
+        return;
+    }
+    if (total > (uint32_t)cap) {
+        if (tid == 0) a.result[b] = 0;
+        return;
+    }
+
+    // ---- EMIT: staging windows of kSStage bytes ----
+    for (uint32_t w0 = 0; w0 < total; w0 += (uint32_t)kSStage) {
+        __syncthreads();   // the index (first window) / the previous window's store is done
+        uint32_t lsrc = 0, ldst = 0, llen = 0;   // this lane's long literal run, if any
+        {
+            uint32_t pe = cover, o = obase;
+            for (int r = 0; r < nrec; r++) {
+                const uint32_t w = S.r.rec[r * kSThreads + tid];
+                uint32_t m = (uint32_t)s0 + (w & 63u), len = (w >> 6) & 1023u;
+                const uint32_t off = w >> 16, e = m + len;
+                if (e <= pe) continue;
+                if (m < pe) {
+                    len = e - pe;
+                    m = pe;
+                    if (len < (uint32_t)kMinMatch) continue;
+                }
+                const int lit = (int)(m - pe), ml = (int)len - 4;
+                put(S, o++, w0, ((uint32_t)(lit < 15 ? lit : 15) << 4) | (uint32_t)(ml < 15 ? ml : 15));
+                if (lit >= 15) o = put_len(S, o, w0, lit);
+                if (lit > kSLongRun) {
+                    lsrc = pe;
+                    ldst = o;
+                    llen = (uint32_t)lit;
+                } else {
+                    for (int i = 0; i < lit; i++) put(S, o + (uint32_t)i, w0, ldsb(S, a0 + pe + (uint32_t)i));
+                }
+                o += (uint32_t)lit;
+                put(S, o++, w0, off & 255u);
+                put(S, o++, w0, off >> 8);
+                if (ml >= 15) o = put_len(S, o, w0, ml);
+                pe = e;
+            }
+            if (tid == kSThreads - 1) {   // the last literals (:732-751)
+                uint32_t o2 = body;
+                put(S, o2++, w0, (uint32_t)(lastrun < 15 ? lastrun : 15) << 4);
+                if (lastrun >= 15) o2 = put_len(S, o2, w0, lastrun);
+                // (a long last run is copied by the wave in the second pass below: a lane
+                // has at most one long run among its own records, the first kept one's)
+                if (lastrun <= kSLongRun)
+                    for (int i = 0; i < lastrun; i++) put(S, o2 + (uint32_t)i, w0, ldsb(S, a0 + cover_all + (uint32_t)i));
+            }
+        }
+        // long literal runs, copied by the whole wave one lane's run at a time
+        for (int pass = 0; pass < 2; pass++) {
+            uint32_t ps = lsrc, pd = ldst, pl = llen;
+            if (pass == 1) {
+                pl = 0;
+                if (tid == kSThreads - 1 && lastrun > kSLongRun) {
+                    ps = cover_all;
+                    pd = body + 1u + (uint32_t)extlen(lastrun);
+                    pl = (uint32_t)lastrun;
+                }
+            }
+            uint64_t mk = wave_ballot(pl > 0);
+            while (mk) {
+                const int j = __builtin_ctzll(mk);
+                mk &= mk - 1;
+                const uint32_t s = lane_val(ps, j), d = lane_val(pd, j), L = lane_val(pl, j);
+                // only the part inside the window
+                const uint32_t lo = d > w0 ? 0u : w0 - d;
+                const uint32_t hi = d + L < w0 + (uint32_t)kSStage ? L : (w0 + (uint32_t)kSStage > d ? w0 + (uint32_t)kSStage - d : 0u);
+                for (uint32_t i = lo + (uint32_t)lane; i < hi; i += 64u)
+                    S.u.stage[d + i - w0] = (uint8_t)ldsb(S, a0 + s + i);
+            }
+        }
+        __syncthreads();
+        // store the window
+        const uint32_t wl = total - w0 < (uint32_t)kSStage ? total - w0 : (uint32_t)kSStage;
+        uint8_t *d = (uint8_t *)dstp + w0;
+        if (((uintptr_t)d & 3u) == 0) {
+            const uint32_t nw = wl >> 2;
+            for (uint32_t i = (uint32_t)tid; i < nw; i += kSThreads)
+                ((uint32_t *)d)[i] = ((const uint32_t *)S.u.stage)[i];
+            for (uint32_t i = (nw << 2) + (uint32_t)tid; i < wl; i += kSThreads) d[i] = S.u.stage[i];
+        } else {
+            for (uint32_t i = (uint32_t)tid; i < wl; i += kSThreads) d[i] = S.u.stage[i];
+        }
+    }
+    if (tid == 0) a.result[b] = (int)total;
+}
+
+hipError_t launch_encode_seg(const BlockArgs &a, hipStream_t s) {
+    if (a.nblocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lz4_encode_seg_kernel, dim3(a.nblocks), dim3(kSThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace apelz4

@@ -146,6 +146,8 @@ hipError_t launch_decode(const BlockArgs &a, bool partial, hipStream_t s);
 // workgroup per connection looping over its chunks in order (lz4_decode.hip)
 hipError_t launch_decode_chain(const BlockArgs &a, int nconn, int nq, hipStream_t s);
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s);
+// the segment-parallel encoder (lz4_encode_seg.hip): acceleration 1, no prefix
+hipError_t launch_encode_seg(const BlockArgs &a, hipStream_t s);
 // compress_destSize pass 2 (lz4_destsize.hip): scratch slot i (at scratch + i*stride, encoder
 // result sres[i]) -> dst[i] cut to target[i]; src_size[i] <- consumed input
 hipError_t launch_destsize(const char *const *src, int *src_size, char *const *dst,
