@@ -61,27 +61,6 @@ constexpr int kWinNeed = 84;     // a parse window reads up to P + 63 + 21
 constexpr int kBatch = 64;       // descriptors per copy batch (one per lane)
 constexpr int kMaxDesc = kBatch + 44;   // held before a copy: <= 63 + 44 (two windows); a third only while nd stays <= kMaxDesc
 constexpr uint32_t kLaneMax = 64;  // longest match one lane copies (4 x 16 bytes)
-#ifndef APE_LZ4_DMUX
-#define APE_LZ4_DMUX 1             // chain_at's lane-bit selects as VGPR-mask muxes (v_bfi)
-#endif
-#ifndef APE_LZ4_DREL
-#define APE_LZ4_DREL 1             // spec compares on staged positions, one b64 read, hop alone
-#endif
-#ifndef APE_LZ4_DFWD
-#define APE_LZ4_DFWD 0             // pending matches forwarded through their owner's offset
-#endif
-#ifndef APE_LZ4_DLOOP1
-#define APE_LZ4_DLOOP1 1           // the parse loop with a single exit
-#endif
-#ifndef APE_LZ4_DJMAX
-#define APE_LZ4_DJMAX 1            // lifting jumps absorb exits with a max
-#endif
-#ifndef APE_LZ4_DWIN3
-#define APE_LZ4_DWIN3 1            // up to three speculative windows per member pass
-#endif
-#ifndef APE_LZ4_DUNITS
-#define APE_LZ4_DUNITS 1           // lane matches load / store only the 16-byte units they need
-#endif
 
 struct __attribute__((aligned(16))) WaveLds {
     // stage first: the parse's ds_read2_b32 (8-bit dword offsets) then needs no address add
@@ -211,9 +190,7 @@ struct Dec {
     int64_t oexit;
     int s0;          // staged window start
     int lane;
-#if APE_LZ4_DMUX
     uint32_t mk[5];  // mk[k]: all ones on lanes with bit k set (chain_at's lifting selects, VGPRs)
-#endif
 };
 
 enum { ST_MORE = 0, ST_DONE = 1, ST_ERR = 2 };
@@ -299,10 +276,8 @@ struct Spec {
     int ipl, ipo, q;                 // first literal byte, after the offset, next token
     bool fin_in, mlerr, cx;          // input ends in the literals / ml bytes run out / complex
     bool mlx;                        // match length nibble 15 (an extension byte follows)
-#if APE_LZ4_DREL
     bool mlover;                     // ipo + kLastLiterals > csize (mlerr = mlx && mlover)
     uint32_t r1;                     // staged position after the literals (s0 + r1 = ipl + lit)
-#endif
 };
 
 template <bool FASTD>
@@ -313,13 +288,8 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
     const uint32_t lit = tok >> 4, mn = tok & 15u;
     const uint32_t r1 = r + 1u + lit;           // offset bytes (then the ml byte)
     const uint32_t a1 = r1 & ~3u;
-#if APE_LZ4_DREL
     const l32x2 w = *(const l32x2 *)&L.stage[a1];   // one ds_read_b64 (any byte address)
     const uint32_t x = funnel(w.y, w.x, r1 & 3u);
-#else
-    const uint32_t x = funnel(*(const uint32_t *)&L.stage[a1 + 4], *(const uint32_t *)&L.stage[a1],
-                              r1 & 3u);
-#endif
     const uint32_t e = (x >> 16) & 0xFFu;
     z.lit = lit;
     z.off = x & 0xFFFFu;
@@ -327,7 +297,6 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
     z.ipo = z.ipl + (int)lit + 2;
     const bool mlx = mn == 15u;
     z.mlx = mlx;
-#if APE_LZ4_DREL
     // on the staged position (s0 + r1 = ipl + lit) against a scalar limit: the same
     // compares (all values far below 2^31), without the absolute positions
     const int lim = D.csize - D.s0;   // scalar
@@ -335,10 +304,6 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
     z.mlover = (int)r1 > lim - 2 - kLastLiterals;                  // ipo + 5 > csize
     z.mlerr = !FASTD && mlx && z.mlover;
     z.r1 = r1;
-#else
-    z.fin_in = !FASTD && (uint32_t)z.ipl + lit + 8u > (uint32_t)D.csize;   // ipl >= 1
-    z.mlerr = !FASTD && mlx && z.ipo + kLastLiterals > D.csize;
-#endif
     z.cx = lit == 15u || (mlx && e == 255u && !z.mlerr);
     z.ml = mlx ? 15u + e : mn;
     z.q = z.ipo + (mlx ? 1 : 0);
@@ -353,16 +318,12 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
 // (lanes [0, cnt)); X = the chain's exit (next token position >= 64, or kHopTerm after a
 // final / failing sequence, kHopCplx before a complex token); lastp = the last member.
 constexpr uint32_t kHopTerm = 0x80u, kHopCplx = 0xC0u;
-#ifndef APE_LZ4_DCHAIN16
-#define APE_LZ4_DCHAIN16 1
-#endif
 template <bool FASTD>
 __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, uint32_t &pos,
                                          int &cnt, uint32_t &X, uint32_t &lastp) {
     // hop and the J_k hold window positions x 4: ds_bpermute's byte address (it uses
     // address bits [7:2] only), so an exit (>= 64, i.e. >= 256 here) needs no mask
     uint32_t hop;
-#if APE_LZ4_DREL
     {
         // the hop alone: mlerr implies fin_in (ipo + 5 = ipl + lit + 7), and the successor
         // relative to P is lane + lit + 3 (+1 with the ml byte)
@@ -370,13 +331,6 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
         const uint32_t qr = (uint32_t)D.lane + z.lit + (z.mlx ? 4u : 3u);
         hop = 4u * (z.cx ? kHopCplx : (z.fin_in ? kHopTerm : qr));
     }
-#else
-    {
-        const Spec z = spec_at<FASTD>(L, D, P, (uint32_t)D.lane);
-        hop = 4u * (z.cx ? kHopCplx : ((z.fin_in || z.mlerr) ? kHopTerm : (uint32_t)(z.q - P)));
-    }
-#endif
-#if APE_LZ4_DJMAX
     // Exits absorb as a max: a real hop moves forward (J[a] > a), and an exit (>= 256) reads
     // some lane's J through the address wrap but max keeps it >= 256.  A jump from a real
     // position whose chain reaches its first exit exactly at the jump's end returns that exit
@@ -387,17 +341,10 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
         const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)J);
         return umax(g, a);
     };
-#else
-    auto jump = [](uint32_t J, uint32_t a) {   // exit values absorb
-        const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)J);
-        return a < 256u ? g : a;
-    };
-#endif
     const uint32_t J1 = jump(hop, hop);
     const uint32_t J2 = jump(J1, J1);
     const uint32_t J3 = jump(J2, J2);
     const uint32_t t = (uint32_t)D.lane;
-#if APE_LZ4_DMUX
     // lane t takes J_k where bit k of t is set: a v_bfi on a per-lane VGPR mask each (the
     // lane masks had been hoisted into SGPR pairs, and the SGPR file spilled them to VGPR
     // lanes: two v_readlane to reload one, inside the parse loop)
@@ -414,33 +361,6 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
         sel = jump(J4, p);
     }
     p = vmux(D.mk[4], sel, p);
-#else
-    uint32_t p = (t & 1u) ? lane_val(hop, 0) : 0u;
-    const uint32_t p2 = jump(J1, p);
-    p = (t & 2u) ? p2 : p;
-    const uint32_t p4 = jump(J2, p);
-    p = (t & 4u) ? p4 : p;
-    const uint32_t p8 = jump(J3, p);
-    p = (t & 8u) ? p8 : p;
-#if APE_LZ4_DCHAIN16
-    // Lanes t < 16 are final now.  The chain has more than 15 members only when its member
-    // 15 exists (a 64-byte window averages ~14 sequences on App. C data); otherwise every
-    // lane t >= 15 holds the exit J^15(0) (exits absorb), and J^16 with its two dependent
-    // ds_bpermute rounds is skipped.
-    const uint32_t p15 = lane_val(p, 15);
-    if (p15 < 256u) {   // wave-uniform
-        const uint32_t J4 = jump(J3, J3);
-        const uint32_t p16 = jump(J4, p);
-        p = (t & 16u) ? p16 : p;
-    } else {
-        p = t >= 16u ? p15 : p;
-    }
-#else
-    const uint32_t J4 = jump(J3, J3);
-    const uint32_t p16 = jump(J4, p);
-    p = (t & 16u) ? p16 : p;
-#endif
-#endif
     p >>= 2;
     pos = t < 32u ? p : kHopTerm;
     cnt = __popcll(wave_ballot(pos < 64u));
@@ -478,14 +398,10 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
         chain_at<FASTD>(L, D, PB, posB, cntB, XB, lastB);
         nmB = cntB - (int)((XB >> 7) & (XB >> 6) & 1u);   // (as nmA)
         PC = PB + (int)XB;
-#if APE_LZ4_DWIN3
         // a third window while the members still fit the wave (<= 41 + 22 lanes) and the
         // descriptors the array (nd + nm <= kMaxDesc), and its bytes are staged
         const bool three = XB < kHopTerm && nmA + nmB <= 41 && nd + nmA + nmB <= kMaxDesc - 22 &&
                            PC - D.s0 + kWinNeed <= kStage;
-#else
-        const bool three = false;
-#endif
         if (three) {
             uint32_t XC, lastC;
             int cntC;
@@ -507,12 +423,10 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const uint64_t M = (1ull << nm) - 1ull;   // nm <= 63
     const bool mem = (int)t < nm;
     uint32_t pos = (int)t < nmA ? posA : (uint32_t)(PB - P) + pB;   // relative to P
-#if APE_LZ4_DWIN3
     if (nmC) {
         const uint32_t pC = bperm(posC, (t - (uint32_t)nmAB) & 63u);
         pos = (int)t < nmAB ? pos : (uint32_t)(PC - P) + pC;
     }
-#endif
 
     // member t = the sequence at P + pos, re-read from the staged bytes
     const Spec z = spec_at<FASTD>(L, D, P, mem ? pos : 0u);
@@ -540,23 +454,13 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
         fm = wave_ballot(fin_in) | wave_ballot((int64_t)cpy > D.oexit);
         badfm = wave_ballot(cpy > ucap) | wave_ballot(iend > (uint32_t)D.csize);
     } else {
-#if APE_LZ4_DREL
         // cpy + 12 > cap as cpy >= a scalar bound; iend != csize on the staged position
         const uint32_t capA = ucap > (uint32_t)kMFLimit - 1u ? ucap - ((uint32_t)kMFLimit - 1u) : 0u;
         fm = wave_ballot(fin_in) | wave_ballot(cpy >= capA);
         badfm = wave_ballot(z.r1 != (uint32_t)(D.csize - D.s0)) | wave_ballot(cpy > ucap);
-#else
-        fm = wave_ballot(fin_in) | wave_ballot(cpy + (uint32_t)kMFLimit > ucap);
-        badfm = wave_ballot(iend != (uint32_t)D.csize) | wave_ballot(cpy > ucap);
-#endif
     }
     const bool fin = lane_in(fm);
-#if APE_LZ4_DREL
     const uint64_t mlm = FASTD ? 0ull : wave_ballot(z.mlx) & wave_ballot(z.mlover);
-#else
-    const uint64_t mlm = FASTD ? 0ull
-                               : wave_ballot(z.mlx) & wave_ballot(z.ipo + kLastLiterals > D.csize);
-#endif
     const bool e_off = (DICT ? cpy + D.dsz : cpy) < off;               // :1375-1376
     // FASTD: the bytes a sequence needs must lie inside the readable bound (the reference
     // has no bound and reads on; here that is an error, never a read past the buffer)
@@ -677,7 +581,6 @@ __device__ __forceinline__ void lane_match(WaveLds &L, const Dec &D, uint32_t ba
     uint8_t *w = L.win + (ma - base);
     const int ps = (int)ma - (int)off;
     const bool big = n >= 16u;
-#if APE_LZ4_DUNITS
     // Only the units a lane needs: unit k (k = 1..3) exists when n > 16 k.  Lanes whose
     // match is shorter issue no load for it, so a gather instruction touches only the lines
     // its active lanes need (the texture path's cost is per line: tools/ubench/gather_rate).
@@ -725,45 +628,6 @@ __device__ __forceinline__ void lane_match(WaveLds &L, const Dec &D, uint32_t ba
     } else {
         lds_put_small<true>(w, v0, n);
     }
-#else
-    // unit offsets: 0, 16, 32, 48 clamped to n - 16 (repeats rewrite the same bytes)
-    const uint32_t t1 = big ? umin(16u, n - 16u) : 0u, t2 = big ? umin(32u, n - 16u) : 0u,
-                   t3 = big ? umin(48u, n - 16u) : 0u;
-    if (off != 0u && off < n) {   // overlaps itself (off >= 16, n > 16): unit after unit
-        const uint8_t *s = L.win + ((uint32_t)ps - base);
-        lds_st16(w, lds16(s));
-        lds_st16(w + t1, lds16(s + t1));
-        lds_st16(w + t2, lds16(s + t2));
-        lds_st16(w + t3, lds16(s + t3));
-        return;
-    }
-    uint4 v0, v1, v2, v3;
-    if (!glb) {   // (offset 0: in-window bytes, zeroed below)
-        const uint8_t *s = L.win + ((uint32_t)ps - base);
-        v0 = lds16(s);
-        v1 = lds16(s + t1);
-        v2 = lds16(s + t2);
-        v3 = lds16(s + t3);
-    } else {
-        // all four loads issued together (t1..t3 are 0 for n <= 16: the same line again);
-        // with the last three under `n > 16` the first one's value was waited for before
-        // the others were issued
-        gcu8 *s = (DICT && ps < 0) ? D.dend + ps : (gcu8 *)D.dst + ps;
-        v0 = gload16_nt(s);
-        v1 = gload16_nt(s + t1);
-        v2 = gload16_nt(s + t2);
-        v3 = gload16_nt(s + t3);
-    }
-    if (off == 0u) v0 = v1 = v2 = v3 = make_uint4(0, 0, 0, 0);
-    if (big) {
-        lds_st16(w, v0);
-        lds_st16(w + t1, v1);
-        lds_st16(w + t2, v2);
-        lds_st16(w + t3, v3);
-    } else {
-        lds_put_small<true>(w, v0, n);
-    }
-#endif
 }
 
 // Per-lane sequence of the batch: literal [o, m) from input ls, match [m, me) at offset off.
@@ -831,49 +695,6 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
         else lds_put_small<false>(w, v, nl);
     }
     // round 1
-#if APE_LZ4_DFWD
-    uint64_t r1m = mpm & lpm & wave_ballot(pe <= (int)S0);
-    uint64_t pm = mpm & ~r1m;
-    // sequences owning [max(ps, S0), pe): k0 = owner(first byte), k1 = owner(last byte),
-    // by binary search over the sequence starts (lanes past the batch hold B1)
-    const uint32_t x0 = (uint32_t)(ps > (int)S0 ? ps : (int)S0), x1 = (uint32_t)(pe - 1);
-    uint32_t k0 = 0, k1 = 0;
-    uint32_t offr = off;
-    bool glbr = glb;
-    if (pm) {
-#pragma unroll
-        for (uint32_t st = 32; st >= 1; st >>= 1) {
-            const uint32_t c0 = k0 + st, c1 = k1 + st;
-            const uint32_t v0 = bperm(q.o, c0), v1 = bperm(q.o, c1);
-            k0 = v0 <= x0 ? c0 : k0;
-            k1 = v1 <= x1 ? c1 : k1;
-        }
-        // Forwarding: a pending match whose sources [ps, pe) lie inside the match of one
-        // earlier sequence k, which copied them from [ps - off_k, pe - off_k), bytes before
-        // that match and before S0 (final: window, dst history or dictionary), reads those
-        // bytes in round 1 -- at offset off + off_k (no self-overlap then: the new sources
-        // end before ma).  ~40 % of the pending matches on App. C data
-        // (profiles/r4_dec_forwarding_counts.txt).
-        const uint32_t mk = bperm(q.m, k0), mek = bperm(q.me, k0), ofk = bperm(q.off, k0);
-        const int psf = ps - (int)ofk, pef = pe0 - (int)ofk;
-        const uint64_t inwf = wave_ballot(psf >= (int)base);
-        uint64_t ingf = wave_ballot(pef <= (int)W.gdone) &
-                        (wave_ballot(nm >= 16u) | wave_ballot(psf + 16 <= D.cap));
-        if (DICT) ingf &= wave_ballot(psf >= 0);
-        const uint64_t indf = DICT ? wave_ballot(psf + (int)umax(nm, 16u) <= 0) : 0ull;
-        const uint64_t fwm = pm & lenm & ~off0m & ~ovlm & wave_ballot(k0 == k1) &
-                             wave_ballot(k0 < (uint32_t)lane) & wave_ballot(ofk != 0u) &
-                             wave_ballot(ps >= (int)mk) & wave_ballot(pe0 <= (int)mek) &
-                             wave_ballot(pef <= (int)mk) & wave_ballot(pef <= (int)S0) &
-                             (inwf | ingf | indf);
-        offr = lane_in(fwm) ? off + ofk : off;
-        glbr = lane_in((fwm & ~inwf) | (~fwm & ~off0m & ~inwm));
-        r1m |= fwm;
-        pm &= ~fwm;
-    }
-    lane_match<DICT>(L, D, base, lane_in(r1m), ma, nm, offr, glbr);
-    if (!pm) return;
-#else
     const uint64_t r1m = mpm & lpm & wave_ballot(pe <= (int)S0);
     lane_match<DICT>(L, D, base, lane_in(r1m), ma, nm, off, glb);
     uint64_t pm = mpm & ~r1m;
@@ -889,25 +710,9 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
         k0 = v0 <= x0 ? c0 : k0;
         k1 = v1 <= x1 ? c1 : k1;
     }
-#endif
     k1 = umin(k1, (uint32_t)lane - 1u);   // (its own literal is written; lane 0 has no needs)
     const uint64_t need = (lane_in(pm) && lane > 0 && k0 <= k1)
                               ? (((2ull << k1) - 1ull) & ~((1ull << k0) - 1ull)) : 0ull;
-#if defined(APE_LZ4_STATS) && defined(APE_LZ4_STATS_FWD)   // (its atomics distort the timers)
-    {   // diagnostic: pending matches whose sources lie inside one owner's match part (not its
-        // literals), and of those, the ones whose bytes the owner copied from before S0 (one
-        // forwarding step through the owner's offset would make them round-1 ready)
-        const uint32_t mk = bperm(q.m, k0), mek = bperm(q.me, k0), ofk = bperm(q.off, k0);
-        const bool one = lane_in(pm) && lane > 0 && k0 == k1 && x0 >= mk && x1 < mek && ofk != 0u;
-        const bool pre = one && x1 - ofk < mk && x1 - ofk < S0 && x0 >= ofk;
-        const uint64_t onem = wave_ballot(one), prem = wave_ballot(pre);
-        if (lane == 0) {
-            atomicAdd(&g_dec_stats[11], (unsigned long long)__popcll(pm));
-            atomicAdd(&g_dec_stats[12], (unsigned long long)__popcll(onem));
-            atomicAdd(&g_dec_stats[13], (unsigned long long)__popcll(prem));
-        }
-    }
-#endif
     uint64_t done = ~pm;   // lanes still pending = pm & ~done
     wave_sync();
     for (;;) {
@@ -1038,13 +843,11 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
     D.oexit = PARTIAL ? a.target[b] : 0;
     if (PARTIAL && D.oexit > (int64_t)D.cap - kMFLimit) D.oexit = (int64_t)D.cap - kMFLimit;
     D.lane = lane;
-#if APE_LZ4_DMUX
     for (int k = 0; k < 5; ++k) {
         uint32_t m = 0u - (((uint32_t)lane >> k) & 1u);
         asm volatile("" : "+v"(m));   // opaque: stays a VGPR mask, not turned back into a select
         D.mk[k] = m;
     }
-#endif
     D.dend = nullptr;
     D.dsz = 0;
     if (DICT) {   // usingDict (:1625-1647): any placement, adjacent or not, reads the same
@@ -1102,7 +905,6 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
     uint32_t cst = 0;        // output position of desc[0]
     for (;;) {
         // ---- PARSE ----
-#if APE_LZ4_DLOOP1
         // one exit (a loop with several breaks was structurised into flag phis: s_mov /
         // s_cselect of 64-bit masks per pass); a complex token may jump far past the staged
         // bytes, which the loop condition then sees.  (restage may now also hold with nd >= 64:
@@ -1113,19 +915,6 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
             if (st == ST_MORE && cplx) st = parse_scalar<PARTIAL, FASTD>(L, D, P, op, nd, result);
         }
         const bool restage = st == ST_MORE && P - D.s0 + kWinNeed > kStage;
-#else
-        bool restage = false;
-        while (st == ST_MORE && nd < kBatch) {
-            if (P - D.s0 + kWinNeed > kStage) { restage = true; break; }
-            bool cplx;
-            st = parse_window<PARTIAL, DICT, FASTD>(L, D, P, op, nd, result, cplx);
-            if (st == ST_MORE && cplx) {
-                st = parse_scalar<PARTIAL, FASTD>(L, D, P, op, nd, result);
-                // a complex token may jump far past the staged bytes
-                if (st == ST_MORE && P - D.s0 + kWinNeed > kStage) { restage = true; break; }
-            }
-        }
-#endif
         STAT(0);
         if (st == ST_ERR) break;
         // ---- COPY: batches of <= 64 descriptors; all of them before a restage (their
@@ -1136,9 +925,7 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
             const uint32_t B1 = nc < nd ? (uint32_t)__builtin_amdgcn_readfirstlane(L.desc[nc].y) : op;
             const bool last = st == ST_DONE && nc == nd;
             uint32_t diag = 0;
-#ifndef APE_DEXP_NOCOPY   // diagnostic: instruction count of the parse alone (no output)
             copy_batch<DICT>(L, D, W, nc, cst, B1, last, diag);
-#endif
             STAT_ADD(3, diag & 0xFFFFu);          // wave passes after round 1
             STAT_ADD(5, (diag >> 16) & 0xFFu);    // coop matches
             STAT_ADD(6, diag >> 24);              // window slides
@@ -1190,150 +977,6 @@ lz4_decode_chain_kernel(BlockArgs a, int nconn, int nq) {
     }
 }
 
-#ifdef APE_LZ4_DEC_COOP
-// ---- Experiment (never the product): two waves per block, pipelined ----
-// Wave 0 parses batch k+1 while wave 1 copies batch k: descriptors move from the parser's
-// LDS to the copier's at a handoff between two workgroup barriers; the copier stages the
-// compressed bytes of its batch's literals itself and owns the output window.
-struct CoopLds {
-    WaveLds p, c;    // parser: stage + descriptors (its window unused); copier: all three
-    uint32_t hdr[4];   // handoff: {nc, B0, B1, flags (1 last, 2 end)}
-};
-
-template <bool PARTIAL, bool DICT, bool FASTD>
-__global__ void __launch_bounds__(128)
-lz4_decode_coop_kernel(BlockArgs a) {
-    __shared__ CoopLds S;
-    const int b = blockIdx.x;
-    const int lane = threadIdx.x & 63;
-    const bool parser = threadIdx.x < 64;
-    Dec D;
-    D.dst = (gu8 *)(a.dst ? a.dst[b] : a.dst_base + (size_t)b * a.dst_stride);
-    if (a.frame_off) {
-        const long long f0 = a.frame_off[b], avail = a.frame_off[b + 1] - f0 - 4;
-        int hdr = -1;
-        gcu8 *f = (gcu8 *)(a.src_base + f0);
-        if (avail >= 0)
-            hdr = (int)((uint32_t)f[0] | ((uint32_t)f[1] << 8) | ((uint32_t)f[2] << 16) |
-                        ((uint32_t)f[3] << 24));
-        if (hdr < 0 || (long long)hdr > avail) {
-            if (threadIdx.x == 0) a.result[b] = -1;
-            return;
-        }
-        D.csize = hdr;
-        D.src = f + 4;
-    } else {
-        D.src = (gcu8 *)(a.src ? a.src[b] : a.src_base + (size_t)b * a.src_stride);
-        D.csize = a.src_size[b];
-    }
-    D.cap = a.dst_cap ? a.dst_cap[b] : (int)a.dst_stride;
-    D.oexit = PARTIAL ? a.target[b] : 0;
-    if (PARTIAL && D.oexit > (int64_t)D.cap - kMFLimit) D.oexit = (int64_t)D.cap - kMFLimit;
-    D.lane = lane;
-#if APE_LZ4_DMUX
-    for (int k = 0; k < 5; ++k) {
-        uint32_t m = 0u - (((uint32_t)lane >> k) & 1u);
-        asm volatile("" : "+v"(m));   // opaque: stays a VGPR mask, not turned back into a select
-        D.mk[k] = m;
-    }
-#endif
-    D.dend = nullptr;
-    D.dsz = 0;
-    if (DICT) {
-        const int ds = a.dict_size[b] > 0 ? a.dict_size[b] : 0;
-        D.dend = (gcu8 *)a.dict[b] + ds;
-        D.dsz = ds < 65536 ? (uint32_t)ds : 65536u;
-    }
-    if (FASTD && (D.cap == 0 || D.csize <= 0)) {
-        if (threadIdx.x == 0) a.result[b] = (D.cap == 0 && D.csize > 0 && D.src[0] == 0) ? 1 : -1;
-        return;
-    }
-    if (D.cap == 0 || D.csize <= 0) {
-        if (threadIdx.x == 0) {
-            int r;
-            if (D.cap == 0) r = (D.csize == 1 && D.src[0] == 0) ? 0 : -1;
-            else r = ((D.src ? D.src[0] : 0u) >= 0xF0) ? -3 : -2;
-            a.result[b] = r;
-        }
-        return;
-    }
-    WaveLds &L = parser ? S.p : S.c;
-    if (lane < 4) *(uint32_t *)&L.stage[kStage + 4 * lane] = 0u;
-    D.s0 = stage_base(D.src, 0);
-    if (parser) stage_load(L, D.src, D.csize, D.s0, lane);
-    wave_sync();
-    if (D.cap < 0) {   // as in lz4_decode_kernel
-        if (parser) {
-            int ip = 0, nd = 0, result = 0;
-            uint32_t op0 = 0;
-            (void)parse_scalar<PARTIAL, FASTD>(L, D, ip, op0, nd, result);
-            if (lane == 0) a.result[b] = result;
-        }
-        return;
-    }
-    if (parser) {
-        int P = 0, nd = 0, result = 0, st = ST_MORE;
-        uint32_t op = 0, cst = 0;
-        for (;;) {
-            while (st == ST_MORE && nd < kBatch) {
-                if (P - D.s0 + kWinNeed > kStage) {
-                    wave_sync();
-                    D.s0 = stage_base(D.src, P);
-                    stage_load(L, D.src, D.csize, D.s0, lane);
-                    wave_sync();
-                }
-                bool cplx;
-                st = parse_window<PARTIAL, DICT, FASTD>(L, D, P, op, nd, result, cplx);
-                if (st == ST_MORE && cplx) st = parse_scalar<PARTIAL, FASTD>(L, D, P, op, nd, result);
-            }
-            wave_sync();
-            const int nc = st == ST_ERR ? 0 : (nd < kBatch ? nd : kBatch);
-            const uint32_t B1 = nc < nd ? (uint32_t)__builtin_amdgcn_readfirstlane(L.desc[nc].y) : op;
-            const bool last = st == ST_DONE && nc == nd;
-            const bool end = st == ST_ERR || last;
-            const uint4 dv = L.desc[lane < nc ? lane : 0];
-            const uint4 cv = L.desc[nc + (lane < nd - nc ? lane : 0)];
-            __syncthreads();   // (1) the copier is done with its descriptors
-            if (lane < nc) S.c.desc[lane] = dv;
-            if (lane == 0) {
-                S.hdr[0] = (uint32_t)nc;
-                S.hdr[1] = cst;
-                S.hdr[2] = B1;
-                S.hdr[3] = (last ? 1u : 0u) | (end ? 2u : 0u);
-            }
-            if (nc < nd && lane < nd - nc) L.desc[lane] = cv;
-            nd -= nc;
-            cst = B1;
-            __syncthreads();   // (2) batch handed over
-            if (end) break;
-        }
-        if (lane == 0) a.result[b] = result;
-    } else {
-        Win W;
-        W.base = 0;
-        W.fl = 0;
-        W.gdone = 0;
-        for (;;) {
-            __syncthreads();   // (1)
-            __syncthreads();   // (2)
-            const int nc = (int)__builtin_amdgcn_readfirstlane(S.hdr[0]);
-            const uint32_t B0 = __builtin_amdgcn_readfirstlane(S.hdr[1]);
-            const uint32_t B1 = __builtin_amdgcn_readfirstlane(S.hdr[2]);
-            const uint32_t fl = __builtin_amdgcn_readfirstlane(S.hdr[3]);
-            const bool last = (fl & 1u) != 0u;
-            if (nc > 0 || last) {
-                if (nc > 0) {   // this batch's literals, staged from its first one on
-                    D.s0 = stage_base(D.src, (int)__builtin_amdgcn_readfirstlane(L.desc[0].x));
-                    stage_load(L, D.src, D.csize, D.s0, lane);
-                }
-                uint32_t diag = 0;
-                copy_batch<DICT>(L, D, W, nc, B0, B1, last, diag);
-            }
-            if (fl & 2u) break;
-        }
-    }
-}
-#endif
 
 hipError_t launch_decode_chain(const BlockArgs &a, int nconn, int nq, hipStream_t s) {
     if (nconn <= 0 || nq <= 0) return hipSuccess;
@@ -1343,12 +986,6 @@ hipError_t launch_decode_chain(const BlockArgs &a, int nconn, int nq, hipStream_
 
 hipError_t launch_decode(const BlockArgs &a, bool partial, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
-#ifdef APE_LZ4_DEC_COOP
-    if (!a.fast && !a.dict && !partial) {
-        hipLaunchKernelGGL((lz4_decode_coop_kernel<false, false, false>), dim3(a.nblocks), dim3(128), 0, s, a);
-        return hipGetLastError();
-    }
-#endif
     if (a.fast)   // decompress_fast (ref :1489)
         hipLaunchKernelGGL((lz4_decode_kernel<false, false, true>), dim3(a.nblocks), dim3(64), 0, s, a);
     else if (a.dict)   // usingDict decodes are full decodes (ref :1625-1647)
