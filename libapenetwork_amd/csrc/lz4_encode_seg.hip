@@ -86,7 +86,8 @@ __device__ __forceinline__ uint32_t sffbl(uint32_t d) {
 // multiplies (v_mul_u32_u24 / v_mad_u32_u24)
 __device__ __forceinline__ uint32_t shash(uint32_t x, uint32_t b4) {
     const uint32_t lo = x & 0xFFFFFFu, hi = (x >> 24) | ((b4 & 0xFFu) << 8);
-    return (__umul24(lo, 0x9E3779u) + __umul24(hi, 0xC2B2AEu)) >> (32 - kSHLog);
+    // (__umul24 returns int: the sum is shifted as unsigned)
+    return ((uint32_t)__umul24(lo, 0x9E3779u) + (uint32_t)__umul24(hi, 0xC2B2AEu)) >> (32 - kSHLog);
 }
 
 // 16 bytes at byte address x of the block buffer: aligned dword reads + v_alignbyte
@@ -115,6 +116,14 @@ __device__ __forceinline__ uint32_t prefix16(uint4 A, uint4 B) {
 }
 
 __device__ __forceinline__ int extlen(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
+
+// Diagnostic build (-DAPE_SEG_GUARD, never the product): every data-dependent loop gets an
+// iteration bound; a tripped bound ends the loop and marks the block's result.
+#ifdef APE_SEG_GUARD
+#define SGUARD(cnt, lim, code) if (++(cnt) > (lim)) { g_trip = (code); break; }
+#else
+#define SGUARD(cnt, lim, code)
+#endif
 
 // block-wide exclusive sum over the 1024 threads; *total = the sum of all
 __device__ __forceinline__ uint32_t block_excl_sum(SegLds &S, uint32_t v, int wave, int lane,
@@ -161,6 +170,7 @@ __device__ __forceinline__ void put(SegLds &S, uint32_t o, uint32_t w0, uint32_t
 // the length bytes after a token nibble of 15: (v - 15) / 255 bytes of 255 and the rest
 __device__ __forceinline__ uint32_t put_len(SegLds &S, uint32_t o, uint32_t w0, int v) {
     v -= 15;
+#pragma unroll 1
     for (; v >= 255; v -= 255) put(S, o++, w0, 255u);
     put(S, o++, w0, (uint32_t)v);
     return o;
@@ -170,6 +180,10 @@ __device__ __forceinline__ uint32_t put_len(SegLds &S, uint32_t o, uint32_t w0, 
 
 __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) {
     __shared__ SegLds S;
+#ifdef APE_SEG_GUARD
+    int g_trip = 0;
+    if (threadIdx.x == 0) S.wmax[15] = 0u;
+#endif
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -204,47 +218,67 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
 
     // ---- INDEX: stable counting sort of positions 4i (4i <= n-13) by hash ----
     const int nidx = n >= 13 ? (n - 13) / kSStride + 1 : 0;
-    uint32_t hv[16];
-#pragma unroll
+#pragma unroll 4
     for (int r = 0; r < 16; r++) {
         const int i = wave * 1024 + r * 64 + lane;
-        hv[r] = kSBuckets;
         if (i < nidx) {
             const uint32_t x = a0 + (uint32_t)(i * kSStride);
-            hv[r] = shash(lds4(S, x), ldsb(S, x + 4));
-            atomicAdd(&S.r.cnt[wave * (kSBuckets / 2) + (hv[r] >> 1)], (hv[r] & 1u) ? 0x10000u : 1u);
+            const uint32_t h = shash(lds4(S, x), ldsb(S, x + 4));
+            atomicAdd(&S.r.cnt[wave * (kSBuckets / 2) + (h >> 1)], (h & 1u) ? 0x10000u : 1u);
         }
     }
     __syncthreads();
     {
         const int h = tid;   // one bucket per thread
-        uint32_t start[kSWaves], run = 0;
-#pragma unroll
-        for (int w = 0; w < kSWaves; w++) {
-            const uint32_t c = (S.r.cnt[w * (kSBuckets / 2) + (h >> 1)] >> ((h & 1) * 16)) & 0xFFFFu;
-            start[w] = run;
-            run += c;
-        }
+        const uint16_t *c16r = (const uint16_t *)S.r.cnt;
+        uint32_t run = 0;
+        for (int w = 0; w < kSWaves; w++) run += c16r[w * kSBuckets + h];
         uint32_t tot;
         const uint32_t base = block_excl_sum(S, run, wave, lane, &tot);
         S.u.ix.offs[h] = base;
         if (h == kSBuckets - 1) S.u.ix.offs[kSBuckets] = tot;
         uint16_t *c16 = (uint16_t *)S.r.cnt;
-#pragma unroll
-        for (int w = 0; w < kSWaves; w++) c16[w * kSBuckets + h] = (uint16_t)(base + start[w]);
+        uint32_t at = base;   // wave w's positions of bucket h start after waves < w's
+        for (int w = 0; w < kSWaves; w++) {
+            const uint32_t c = c16[w * kSBuckets + h];
+            c16[w * kSBuckets + h] = (uint16_t)at;
+            at += c;
+        }
     }
     __syncthreads();
-#pragma unroll
+#pragma unroll 1
     for (int r = 0; r < 16; r++) {   // in order: a wave's positions enter each bucket ascending
-        if (hv[r] < (uint32_t)kSBuckets) {
-            const uint32_t old = atomicAdd(&S.r.cnt[wave * (kSBuckets / 2) + (hv[r] >> 1)],
-                                           (hv[r] & 1u) ? 0x10000u : 1u);
-            const uint32_t slot = (old >> ((hv[r] & 1u) * 16)) & 0xFFFFu;
-            S.u.ix.pos[slot] = (uint16_t)((wave * 1024 + r * 64 + lane) * kSStride);
+        const int i = wave * 1024 + r * 64 + lane;
+        if (i < nidx) {
+            const uint32_t x = a0 + (uint32_t)(i * kSStride);
+            const uint32_t h = shash(lds4(S, x), ldsb(S, x + 4));
+            const uint32_t old = atomicAdd(&S.r.cnt[wave * (kSBuckets / 2) + (h >> 1)],
+                                           (h & 1u) ? 0x10000u : 1u);
+            const uint32_t slot = (old >> ((h & 1u) * 16)) & 0xFFFFu;
+#ifdef APE_SEG_GUARD
+            if (slot >= (uint32_t)nidx) atomicOr(&S.wmax[15], 1u << 5);
+#endif
+            S.u.ix.pos[slot] = (uint16_t)(i * kSStride);
         }
     }
     __syncthreads();
 
+#ifdef APE_SEG_GUARD
+    {   // diagnostic: index consistency (bits of the block's result)
+        int bad = 0;
+        const uint32_t o0 = S.u.ix.offs[tid], o1 = S.u.ix.offs[tid + 1];
+        if (o1 < o0) atomicOr(&S.wmax[15], 1u << 1);
+        if (tid == 0 && S.u.ix.offs[kSBuckets] != (uint32_t)nidx) atomicOr(&S.wmax[15], 1u << 2);
+        for (uint32_t k = o0 + 1; k < o1 && k < (uint32_t)kSIdx; k++)
+            bad += S.u.ix.pos[k] <= S.u.ix.pos[k - 1];
+        if (bad) atomicOr(&S.wmax[15], 1u << 3);
+        for (uint32_t k = o0; k < o1 && k < (uint32_t)kSIdx; k++)
+            if (shash(lds4(S, a0 + S.u.ix.pos[k]), ldsb(S, a0 + S.u.ix.pos[k] + 4)) != (uint32_t)tid) { atomicOr(&S.wmax[15], 1u << 4); break; }
+        __syncthreads();
+        if (S.wmax[15]) g_trip = 100 + (int)S.wmax[15];
+        __syncthreads();
+    }
+#endif
     // ---- PARSE: lane tid, segment [s0, s1) ----
     const int s0 = tid * kSSeg;
     const int mfl = n - 12;                  // matches start at <= n-12 (:585)
@@ -255,12 +289,16 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
         // segment's coverage ends then still starts at <= n-12
         const int capE = s1 + kSCapX < mfl ? s1 + kSCapX : mfl;
         int q = s0 > 1 ? s0 : 1, anchor = s0;
+        int gp = 0;
         while (q < s1 && q <= mfl && nrec < kSRec) {
+            SGUARD(gp, 200, 1)
             const uint4 own = lds16(S, a0 + (uint32_t)q);
             const uint32_t h = shash(own.x, own.y);
             int lo = (int)S.u.ix.offs[h], hi = (int)S.u.ix.offs[h + 1];
             const int blo = lo;
+            int gb = 0;
             while (lo < hi) {   // first entry >= q
+                SGUARD(gb, 40, 2)
                 const int mid = (lo + hi) >> 1;
                 if ((int)S.u.ix.pos[mid] < q) lo = mid + 1;
                 else hi = mid;
@@ -270,8 +308,8 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
 #pragma unroll
             for (int d = 0; d < kSDepth; d++) {
                 const int j = lo - 1 - d;
-                if (j >= blo) {
-                    const int c = (int)S.u.ix.pos[j];
+                const int c = j >= blo ? (int)S.u.ix.pos[j] : q;
+                if (c < q) {
                     int l = (int)prefix16(own, lds16(S, a0 + (uint32_t)c));
                     l = l < room ? l : room;
                     if (l > best) { best = l; bestc = c; }
@@ -280,7 +318,9 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
             if (best < kMinMatch) { q++; continue; }
             int len = best;
             if (best == 16) {
+                int ge = 0;
                 while (len < room) {
+                    SGUARD(ge, 40, 3)
                     const int l = (int)prefix16(lds16(S, a0 + (uint32_t)(q + len)),
                                                 lds16(S, a0 + (uint32_t)(bestc + len)));
                     len += l;
@@ -289,7 +329,9 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
                 len = len < room ? len : room;
             }
             int m = q, c = bestc;   // catch-up (:623-627)
+            int gc = 0;
             while (m > anchor && c > 0 && ldsb(S, a0 + (uint32_t)(m - 1)) == ldsb(S, a0 + (uint32_t)(c - 1))) {
+                SGUARD(gc, 80, 4)
                 m--;
                 c--;
                 len++;
@@ -304,47 +346,60 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
     // ---- SPLICE: where each segment's kept sequences start; sizes; output offsets ----
     // Coverage after segment k: C_k = f_k(C_{k-1}), f_k(c) = c + 4 <= e_k ? e_k : c with e_k
     // the end of k's last match (a match cut to start at c is kept only if >= 4 bytes; all
-    // of k's earlier matches end before its last one starts).  C is the fixed point of
-    // cover = exclusive-prefix-max(f(cover)), reached from the plain prefix max of e in one
-    // or two rounds (a cut < 4 bytes is rare); a sequential pass settles the rest.
+    // of k's earlier matches end before its last one starts).  Scanned as keys e << 10 | k of
+    // the segments that produce coverage (0 for the others), so that the exclusive prefix max
+    // also names the producer.  C is the fixed point of key = excl-prefix-max(f(key)), reached
+    // from the plain prefix max of e in one or two rounds (a cut < 4 bytes is rare); a
+    // sequential pass settles the rest.
     uint32_t elast = 0;
     if (nrec > 0) {
         const uint32_t r = S.r.rec[(nrec - 1) * kSThreads + tid];
         elast = (uint32_t)s0 + (r & 63u) + ((r >> 6) & 1023u);
     }
-    uint32_t cover_all;
-    uint32_t cover = block_excl_max(S, elast, wave, lane, &cover_all);
+    const uint32_t key0 = nrec > 0 ? (elast << 10) | (uint32_t)tid : 0u;
+    uint32_t allk;
+    uint32_t ck = block_excl_max(S, key0, wave, lane, &allk);
     for (int it = 0;; it++) {
-        const uint32_t E = cover + 4u <= elast ? elast : cover;
+        const uint32_t E = (ck >> 10) + 4u <= elast ? key0 : 0u;
         uint32_t all2;
         const uint32_t c2 = block_excl_max(S, E, wave, lane, &all2);
-        const bool moved = c2 != cover;
-        cover = c2;
-        cover_all = all2;
+        const bool moved = c2 != ck;
+        ck = c2;
+        allk = all2;
         if (!__syncthreads_or(moved)) break;
         if (it == 3) {   // sequential: thread 0 walks the segments (ends in LDS)
             uint32_t *ends = (uint32_t *)S.u.stage;
             ends[tid] = elast;
             __syncthreads();
             if (tid == 0) {
-                uint32_t c = 0;
+                uint32_t c = 0, kk = 0;
                 for (int k = 0; k < kSThreads; k++) {
                     const uint32_t e = ends[k];
-                    ends[k] = c;
-                    if (c + 4u <= e) c = e;
+                    ends[k] = kk;
+                    if ((kk >> 10) + 4u <= e) kk = (e << 10) | (uint32_t)k;
+                    c = kk;
                 }
                 S.wmax[0] = c;
             }
             __syncthreads();
-            cover = ends[tid];
-            cover_all = S.wmax[0];
+            ck = ends[tid];
+            allk = S.wmax[0];
             __syncthreads();
             break;
         }
     }
-    uint32_t sz = 0;
+    const uint32_t cover = ck >> 10, cover_all = allk >> 10;
+
+    // Runs longer than a segment: a kept match that starts exactly where the coverage ends,
+    // at the offset of the match that ends there, continues that match (every 64 bytes of a
+    // long run are found again by the next segment).  It is folded into its head sequence:
+    // T_k = val_k + (pass_k ? T_{k+1} : 0) sums the continuations after segment k (val = the
+    // continuing length, pass = the segment holds nothing else, so the chain goes on), a
+    // segmented suffix scan; the head (a segment's last kept match) takes T_{k+1} on top.
+    uint32_t kc = 0, f_m = 0, f_len = 0, f_off = 0, l_off = 0;
     {
         uint32_t pe = cover;
+#pragma unroll 1
         for (int r = 0; r < nrec; r++) {
             const uint32_t w = S.r.rec[r * kSThreads + tid];
             uint32_t m = (uint32_t)s0 + (w & 63u), len = (w >> 6) & 1023u;
@@ -355,11 +410,72 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
                 m = pe;
                 if (len < (uint32_t)kMinMatch) continue;
             }
-            const int lit = (int)(m - pe);
-            sz += 1u + (uint32_t)extlen(lit) + (uint32_t)lit + 2u + (uint32_t)extlen((int)len - 4);
+            if (kc == 0) { f_m = m; f_len = len; f_off = w >> 16; }
+            l_off = w >> 16;
+            kc++;
             pe = e;
         }
     }
+    uint32_t *segoff = (uint32_t *)S.u.stage;            // [1024] last kept offset
+    uint32_t *segvp = segoff + kSThreads;                 // [1024] val | !pass << 31
+    uint32_t *segT = segvp + kSThreads;                   // [1025] T_k
+    segoff[tid] = l_off;
+    __syncthreads();
+    const bool cont = kc > 0 && ck != 0u && f_m == cover && f_off == segoff[ck & 1023u];
+    const uint32_t val = cont ? f_len : 0u;
+    const bool pass = kc == 0 || (cont && kc == 1);
+    segvp[tid] = val | (pass ? 0u : 0x80000000u);
+    if (tid == 0) segT[kSThreads] = 0u;
+    __syncthreads();
+    {   // thread t scans segment 1023 - t: S_t = x_t + (reset_t ? 0 : S_{t-1})
+        const uint32_t vp = segvp[kSThreads - 1 - tid];
+        uint32_t x = vp & 0x7FFFFFFFu, fl = vp >> 31;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {   // wave segmented scan (flag, value) pairs
+            const uint32_t px = __shfl_up(x, d), pf = __shfl_up(fl, d);
+            if (lane >= d) {
+                x = fl ? x : x + px;
+                fl |= pf;
+            }
+        }
+        // carry across waves: wave w's lanes without a reset before them take the previous
+        // waves' running value (sequential over the 16 wave totals in LDS)
+        if (lane == 63) {
+            S.wsum[wave] = x;
+            S.wmax[wave] = fl;
+        }
+        __syncthreads();
+        uint32_t carry = 0;
+        for (int w = 0; w < wave; w++) carry = S.wmax[w] ? S.wsum[w] : carry + S.wsum[w];
+        if (!fl) x += carry;
+        segT[kSThreads - 1 - tid] = x;
+        __syncthreads();
+    }
+    const uint32_t tail = segT[tid + 1];   // T_{k+1}
+    uint32_t sz = 0;
+    {
+        uint32_t pe = cover, k = 0;
+#pragma unroll 1
+        for (int r = 0; r < nrec; r++) {
+            const uint32_t w = S.r.rec[r * kSThreads + tid];
+            uint32_t m = (uint32_t)s0 + (w & 63u), len = (w >> 6) & 1023u;
+            const uint32_t e = m + len;
+            if (e <= pe) continue;
+            if (m < pe) {
+                len = e - pe;
+                m = pe;
+                if (len < (uint32_t)kMinMatch) continue;
+            }
+            k++;
+            if (!(k == 1 && cont)) {   // a continuation's bytes are its head's
+                const uint32_t L = len + (k == kc ? tail : 0u);
+                const int lit = (int)(m - pe);
+                sz += 1u + (uint32_t)extlen(lit) + (uint32_t)lit + 2u + (uint32_t)extlen((int)L - 4);
+            }
+            pe = e;
+        }
+    }
+    __syncthreads();   // segT / segvp (stage area) read before the emission writes it
     uint32_t body;
     const uint32_t obase = block_excl_sum(S, sz, wave, lane, &body);
     const int lastrun = n - (int)cover_all;
@@ -386,11 +502,13 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
     }
 
     // ---- EMIT: staging windows of kSStage bytes ----
+#pragma unroll 1
     for (uint32_t w0 = 0; w0 < total; w0 += (uint32_t)kSStage) {
         __syncthreads();   // the index (first window) / the previous window's store is done
         uint32_t lsrc = 0, ldst = 0, llen = 0;   // this lane's long literal run, if any
         {
-            uint32_t pe = cover, o = obase;
+            uint32_t pe = cover, o = obase, k = 0;
+#pragma unroll 1
             for (int r = 0; r < nrec; r++) {
                 const uint32_t w = S.r.rec[r * kSThreads + tid];
                 uint32_t m = (uint32_t)s0 + (w & 63u), len = (w >> 6) & 1023u;
@@ -401,6 +519,12 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
                     m = pe;
                     if (len < (uint32_t)kMinMatch) continue;
                 }
+                k++;
+                if (k == 1 && cont) {   // continuation: written with its head
+                    pe = e;
+                    continue;
+                }
+                if (k == kc) len += tail;
                 const int lit = (int)(m - pe), ml = (int)len - 4;
                 put(S, o++, w0, ((uint32_t)(lit < 15 ? lit : 15) << 4) | (uint32_t)(ml < 15 ? ml : 15));
                 if (lit >= 15) o = put_len(S, o, w0, lit);
@@ -409,6 +533,7 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
                     ldst = o;
                     llen = (uint32_t)lit;
                 } else {
+#pragma unroll 1
                     for (int i = 0; i < lit; i++) put(S, o + (uint32_t)i, w0, ldsb(S, a0 + pe + (uint32_t)i));
                 }
                 o += (uint32_t)lit;
@@ -424,10 +549,12 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
                 // (a long last run is copied by the wave in the second pass below: a lane
                 // has at most one long run among its own records, the first kept one's)
                 if (lastrun <= kSLongRun)
+#pragma unroll 1
                     for (int i = 0; i < lastrun; i++) put(S, o2 + (uint32_t)i, w0, ldsb(S, a0 + cover_all + (uint32_t)i));
             }
         }
         // long literal runs, copied by the whole wave one lane's run at a time
+#pragma unroll 1
         for (int pass = 0; pass < 2; pass++) {
             uint32_t ps = lsrc, pd = ldst, pl = llen;
             if (pass == 1) {
@@ -446,6 +573,7 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
                 // only the part inside the window
                 const uint32_t lo = d > w0 ? 0u : w0 - d;
                 const uint32_t hi = d + L < w0 + (uint32_t)kSStage ? L : (w0 + (uint32_t)kSStage > d ? w0 + (uint32_t)kSStage - d : 0u);
+#pragma unroll 1
                 for (uint32_t i = lo + (uint32_t)lane; i < hi; i += 64u)
                     S.u.stage[d + i - w0] = (uint8_t)ldsb(S, a0 + s + i);
             }
@@ -463,6 +591,10 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
             for (uint32_t i = (uint32_t)tid; i < wl; i += kSThreads) d[i] = S.u.stage[i];
         }
     }
+#ifdef APE_SEG_GUARD
+    if (g_trip) a.result[b] = -1000000 - g_trip * 1000 - (tid & 1023) * 0;
+    else
+#endif
     if (tid == 0) a.result[b] = (int)total;
 }
 

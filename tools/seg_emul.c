@@ -96,30 +96,40 @@ static int encode(const uint8_t *src, int n, uint8_t *out)
         if (it > wmax) wmax = it;
         if ((t & 63) == 63) { g_wave_iters += wmax; wmax = 0; }
     }
-    /* splice + emit (sequential over lanes: same arithmetic as the kernel) */
+    /* splice (sequential over lanes: the kernel's rules) -> sequences, then emit */
+    static uint32_t sq_m[65536], sq_len[65536], sq_off[65536], sq_lit0[65536];
+    int ns = 0;
     uint32_t cover = 0;
-    int o = 0;
     for (int t = 0; t < THREADS; t++) {
         uint32_t pe = cover;
-        int s0 = t * SEG;
+        int s0 = t * SEG, k = 0;
         for (int r = 0; r < nrec[t]; r++) {
             uint32_t w = rec[t][r], m = s0 + (w & 63), len = (w >> 6) & 1023, off = w >> 16, e = m + len;
             if (e <= pe) continue;
             if (m < pe) { len = e - pe; m = pe; if (len < 4) continue; }
-            int lit = m - pe, ml = len - 4;
-            out[o++] = (uint8_t)(((lit < 15 ? lit : 15) << 4) | (ml < 15 ? ml : 15));
-            if (lit >= 15) { int v = lit - 15; for (; v >= 255; v -= 255) out[o++] = 255; out[o++] = v; }
-            memcpy(out + o, blk + pe, lit);
-            o += lit;
-            out[o++] = off & 255;
-            out[o++] = off >> 8;
-            if (ml >= 15) { int v = ml - 15; for (; v >= 255; v -= 255) out[o++] = 255; out[o++] = v; }
+            k++;
+            if (k == 1 && ns > 0 && m == cover && sq_m[ns - 1] + sq_len[ns - 1] == cover && off == sq_off[ns - 1]) {
+                sq_len[ns - 1] += len;   /* continuation of the covering match */
+            } else {
+                sq_lit0[ns] = pe; sq_m[ns] = m; sq_len[ns] = len; sq_off[ns] = off; ns++;
+            }
             pe = e;
         }
         if (nrec[t]) {   /* coverage after this segment: f(c) = c + 4 <= e ? e : c */
             uint32_t w = rec[t][nrec[t] - 1], e = s0 + (w & 63) + ((w >> 6) & 1023);
             if (cover + 4 <= e) cover = e;
         }
+    }
+    int o = 0;
+    for (int i = 0; i < ns; i++) {
+        int lit = sq_m[i] - sq_lit0[i], ml = sq_len[i] - 4;
+        out[o++] = (uint8_t)(((lit < 15 ? lit : 15) << 4) | (ml < 15 ? ml : 15));
+        if (lit >= 15) { int v = lit - 15; for (; v >= 255; v -= 255) out[o++] = 255; out[o++] = v; }
+        memcpy(out + o, blk + sq_lit0[i], lit);
+        o += lit;
+        out[o++] = sq_off[i] & 255;
+        out[o++] = sq_off[i] >> 8;
+        if (ml >= 15) { int v = ml - 15; for (; v >= 255; v -= 255) out[o++] = 255; out[o++] = v; }
     }
     int last = n - cover;
     out[o++] = (uint8_t)((last < 15 ? last : 15) << 4);
@@ -153,6 +163,7 @@ int main(int argc, char **argv)
         for (int b = 0; b < nb; b++) {
             const uint8_t *s = in + (size_t)b * n;
             int c = encode(s, n, out);
+            if (b < 4) printf("block %d: %d\n", b, c);
             tot += c;
             rtot += cmp((const char *)s, (char *)rout, n, 70000);
             int r = dec((const char *)out, (char *)back, c, n);
@@ -171,6 +182,7 @@ int main(int argc, char **argv)
         uint8_t *s = in;
         for (int i = 0; i < m; i++) s[i] = (k % 3 == 0) ? 0 : (k % 3 == 1) ? (uint8_t)(i % 7) : in[i];
         int c = encode(s, m, out);
+        if (k == 3 || k == 6) printf("size %d content %d: %d bytes\n", m, k % 3, c);
         int r = dec((const char *)out, (char *)back, c, m);
         if (r != m || memcmp(back, s, m)) { bad++; if (bad < 5) printf("bad size %d r %d c %d\n", m, r, c); }
     }
