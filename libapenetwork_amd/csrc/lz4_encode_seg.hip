@@ -43,18 +43,37 @@
 
 namespace apelz4 {
 
+#ifdef APE_LZ4_STATS
+__device__ unsigned long long g_seg_stats[16];
+// per-phase cycle sums of the segment encoder (workgroup thread 0, barrier to barrier)
+hipError_t seg_stats_read(unsigned long long *out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg_stats), sizeof(g_seg_stats));
+    if (e == hipSuccess && reset) {
+        unsigned long long z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg_stats), z, sizeof(z));
+    }
+    return e;
+}
+#endif
+
 namespace {
 
-constexpr int kSThreads = 1024, kSWaves = kSThreads / 64;
-constexpr int kSSeg = kMaxBlock / kSThreads;     // 64 bytes per segment (lane)
+constexpr int kSThreads = 1024, kSWaves = kSThreads / 64, kSHalf = kSWaves / 2;
+constexpr int kSSeg = 16;                         // bytes per segment (a lane's unit of work)
+constexpr int kSSegs = kMaxBlock / kSSeg;         // 4096 segments
+constexpr int kSWaveSegs = kSSegs / kSWaves;      // 256 segments (4 KiB) per wave
+constexpr int kSRecS = 3;                         // record slots per segment
 constexpr int kSStride = 4;                       // indexed positions: multiples of 4
-constexpr int kSHLog = 10, kSBuckets = 1 << kSHLog;
+constexpr int kSHLog = 11, kSBuckets = 1 << kSHLog;
 constexpr int kSIdx = kMaxBlock / kSStride;       // 16384 index entries
 constexpr int kSCapX = 64;                        // a match may end this far past its segment
-constexpr int kSRec = 14;                         // record slots per segment
-constexpr int kSDepth = 4;                        // candidates measured per position
+#ifndef APE_SEG_DEPTH
+#define APE_SEG_DEPTH 4
+#endif
+constexpr int kSDepth = APE_SEG_DEPTH;            // candidates measured per position
 constexpr int kSLongRun = 64;                     // longer literal runs: copied by the wave
-constexpr int kSBlkW = (kMaxBlock + 64) / 4;      // block bytes at offset a (< 16) + padding
+constexpr int kSFront = 16;                       // zero bytes before the block (backward reads)
+constexpr int kSBlkW = (kSFront + kMaxBlock + 64) / 4;   // block bytes at kSFront + a (a < 16) + padding
 
 struct SegLds {
     uint32_t blk[kSBlkW];
@@ -66,15 +85,18 @@ struct SegLds {
         uint8_t stage[kSIdx * 2 + (kSBuckets + 1) * 4];
     } u;
     union {
-        uint32_t cnt[kSWaves * kSBuckets / 2];    // index build: per-wave u16 counters, packed
-        uint32_t rec[kSRec * kSThreads];          // parse: record r of lane k at [r*1024 + k]
+        struct {                                  // index build, one half of the waves at a time:
+            uint32_t cnt[kSHalf * kSBuckets / 2]; // per-wave u16 bucket counters, packed in pairs
+            uint32_t tot[kSBuckets];              // bucket totals, then the second half's starts
+        } ib;
+        uint32_t rec[kSRecS * kSSegs];            // parse: slot r of segment g at [r*4096 + g]
     } r;
     uint32_t wsum[kSWaves];
     uint32_t wmax[kSWaves];
 };
 constexpr int kSStage = (int)sizeof(((SegLds *)0)->u.stage) & ~15;
 static_assert(sizeof(SegLds) <= 160 * 1024, "LDS");
-static_assert(kSSeg == 64, "segment = 64 bytes (record start field: 6 bits)");
+static_assert(kSSeg == 16 && kSThreads * 4 == kSSegs, "a thread's 64-byte region = 4 segments (start field: 4 bits)");
 
 __device__ __forceinline__ uint32_t sffbl(uint32_t d) {
     uint32_t r;
@@ -90,7 +112,9 @@ __device__ __forceinline__ uint32_t shash(uint32_t x, uint32_t b4) {
     return ((uint32_t)__umul24(lo, 0x9E3779u) + (uint32_t)__umul24(hi, 0xC2B2AEu)) >> (32 - kSHLog);
 }
 
-// 16 bytes at byte address x of the block buffer: aligned dword reads + v_alignbyte
+// 16 / 4 bytes at byte address x of the block buffer.  Default: single unaligned LDS reads
+// (gfx950 serves any alignment); APE_SEG_ALIGNED_READS: aligned dword reads + v_alignbyte.
+#ifdef APE_SEG_ALIGNED_READS
 __device__ __forceinline__ uint4 lds16(const SegLds &S, uint32_t x) {
     const uint32_t *r = S.blk + (x >> 2);
     const uint32_t sh = x & 3u;
@@ -102,6 +126,19 @@ __device__ __forceinline__ uint32_t lds4(const SegLds &S, uint32_t x) {
     const uint32_t *r = S.blk + (x >> 2);
     return __builtin_amdgcn_alignbyte(r[1], r[0], x & 3u);
 }
+#else
+typedef uint32_t l32x4 __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t l32x4a2 __attribute__((ext_vector_type(4), aligned(2)));
+typedef uint32_t l32 __attribute__((aligned(1)));
+typedef uint32_t l32x2 __attribute__((ext_vector_type(2), aligned(1)));
+__device__ __forceinline__ uint4 lds16(const SegLds &S, uint32_t x) {
+    const l32x4 v = *(const l32x4 *)((const uint8_t *)S.blk + x);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t lds4(const SegLds &S, uint32_t x) {
+    return *(const l32 *)((const uint8_t *)S.blk + x);
+}
+#endif
 __device__ __forceinline__ uint32_t ldsb(const SegLds &S, uint32_t x) {
     return ((const uint8_t *)S.blk)[x];
 }
@@ -180,6 +217,7 @@ __device__ __forceinline__ uint32_t put_len(SegLds &S, uint32_t o, uint32_t w0, 
 
 __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) {
     __shared__ SegLds S;
+    STATS_DECL
 #ifdef APE_SEG_GUARD
     int g_trip = 0;
     if (threadIdx.x == 0) S.wmax[15] = 0u;
@@ -197,192 +235,398 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
     }
 
     // ---- LOAD: the 16-byte-aligned chunks that hold the block's bytes; byte i of the
-    // block lands at blk byte a0 + i.  Chunks outside the block are never read (a chunk
+    // block lands at blk byte a0 = 16 + a + i.  Chunks outside the block are never read (a chunk
     // with one valid byte lies in the same page as that byte); the padding is zeroed.
-    const uint32_t a0 = (uint32_t)((uintptr_t)srcp & 15u);
+    const uint32_t amis = (uint32_t)((uintptr_t)srcp & 15u);
+    const uint32_t a0 = (uint32_t)kSFront + amis;   // blk byte of block byte 0
     {
-        const u32x4_u *g = (const u32x4_u *)(srcp - a0);
-        const int nch = n > 0 ? (int)((a0 + (uint32_t)n + 15u) >> 4) : 0;
+        const u32x4_u *g = (const u32x4_u *)(srcp - amis);
+        const int nch = n > 0 ? (int)((amis + (uint32_t)n + 15u) >> 4) : 0;
         uint4 *L = (uint4 *)S.blk;
         for (int c = tid; c < kSBlkW / 4; c += kSThreads) {
             uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if (c < nch) {
-                const u32x4_u t = __builtin_nontemporal_load(g + c);
+            const int gc = c - kSFront / 16;
+            if (gc >= 0 && gc < nch) {
+                const u32x4_u t = __builtin_nontemporal_load(g + gc);
                 v = make_uint4(t.x, t.y, t.z, t.w);
             }
             L[c] = v;
         }
-        for (int i = tid; i < kSWaves * kSBuckets / 2; i += kSThreads) S.r.cnt[i] = 0u;
+        for (int i = tid; i < kSHalf * kSBuckets / 2 + kSBuckets; i += kSThreads) S.r.ib.cnt[i] = 0u;
     }
     __syncthreads();
 
+    STAT(0);
     // ---- INDEX: stable counting sort of positions 4i (4i <= n-13) by hash ----
+    // Wave w holds index entries [1024w, 1024w + 1024).  Bucket totals first; then, one half
+    // of the waves at a time (the per-wave counters of all 16 waves do not fit beside the
+    // rest), per-wave counts -> per-wave starts -> each wave scatters its own entries in
+    // order.  No two waves update one counter, and a wave's atomics on one counter return in
+    // lane order, so every bucket lists its positions in ascending order, deterministically.
     const int nidx = n >= 13 ? (n - 13) / kSStride + 1 : 0;
+    uint16_t *c16 = (uint16_t *)S.r.ib.cnt;
+    const bool first_half = wave < kSHalf;
+    const int hw = wave & (kSHalf - 1);
 #pragma unroll 4
     for (int r = 0; r < 16; r++) {
         const int i = wave * 1024 + r * 64 + lane;
         if (i < nidx) {
             const uint32_t x = a0 + (uint32_t)(i * kSStride);
             const uint32_t h = shash(lds4(S, x), ldsb(S, x + 4));
-            atomicAdd(&S.r.cnt[wave * (kSBuckets / 2) + (h >> 1)], (h & 1u) ? 0x10000u : 1u);
+            atomicAdd(&S.r.ib.tot[h], 1u);
+            if (first_half) atomicAdd(&S.r.ib.cnt[hw * (kSBuckets / 2) + (h >> 1)], (h & 1u) ? 0x10000u : 1u);
         }
     }
     __syncthreads();
-    {
-        const int h = tid;   // one bucket per thread
-        const uint16_t *c16r = (const uint16_t *)S.r.cnt;
-        uint32_t run = 0;
-        for (int w = 0; w < kSWaves; w++) run += c16r[w * kSBuckets + h];
-        uint32_t tot;
-        const uint32_t base = block_excl_sum(S, run, wave, lane, &tot);
-        S.u.ix.offs[h] = base;
-        if (h == kSBuckets - 1) S.u.ix.offs[kSBuckets] = tot;
-        uint16_t *c16 = (uint16_t *)S.r.cnt;
-        uint32_t at = base;   // wave w's positions of bucket h start after waves < w's
-        for (int w = 0; w < kSWaves; w++) {
-            const uint32_t c = c16[w * kSBuckets + h];
-            c16[w * kSBuckets + h] = (uint16_t)at;
-            at += c;
+    {   // bucket starts (two buckets per thread), then the first half's per-wave starts
+        const int h0 = 2 * tid;
+        const uint32_t t0 = S.r.ib.tot[h0], t1 = S.r.ib.tot[h0 + 1];
+        uint32_t all;
+        const uint32_t base = block_excl_sum(S, t0 + t1, wave, lane, &all);
+        S.u.ix.offs[h0] = base;
+        S.u.ix.offs[h0 + 1] = base + t0;
+        if (tid == kSThreads - 1) S.u.ix.offs[kSBuckets] = all;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int h = h0 + k;
+            uint32_t at = base + (k ? t0 : 0u);
+#pragma unroll
+            for (int w = 0; w < kSHalf; w++) {
+                const uint32_t c = c16[w * kSBuckets + h];
+                c16[w * kSBuckets + h] = (uint16_t)at;
+                at += c;
+            }
+            S.r.ib.tot[h] = at;   // where the second half's entries of bucket h begin
         }
     }
     __syncthreads();
 #pragma unroll 1
-    for (int r = 0; r < 16; r++) {   // in order: a wave's positions enter each bucket ascending
-        const int i = wave * 1024 + r * 64 + lane;
-        if (i < nidx) {
-            const uint32_t x = a0 + (uint32_t)(i * kSStride);
-            const uint32_t h = shash(lds4(S, x), ldsb(S, x + 4));
-            const uint32_t old = atomicAdd(&S.r.cnt[wave * (kSBuckets / 2) + (h >> 1)],
-                                           (h & 1u) ? 0x10000u : 1u);
-            const uint32_t slot = (old >> ((h & 1u) * 16)) & 0xFFFFu;
-#ifdef APE_SEG_GUARD
-            if (slot >= (uint32_t)nidx) atomicOr(&S.wmax[15], 1u << 5);
-#endif
-            S.u.ix.pos[slot] = (uint16_t)(i * kSStride);
+    for (int half = 0; half < 2; half++) {
+        if (half == 1) {   // per-wave counts of the second half
+            for (int i = tid; i < kSHalf * kSBuckets / 2; i += kSThreads) S.r.ib.cnt[i] = 0u;
+            __syncthreads();
+            if (!first_half) {
+#pragma unroll 4
+                for (int r = 0; r < 16; r++) {
+                    const int i = wave * 1024 + r * 64 + lane;
+                    if (i < nidx) {
+                        const uint32_t x = a0 + (uint32_t)(i * kSStride);
+                        const uint32_t h = shash(lds4(S, x), ldsb(S, x + 4));
+                        atomicAdd(&S.r.ib.cnt[hw * (kSBuckets / 2) + (h >> 1)], (h & 1u) ? 0x10000u : 1u);
+                    }
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int h = 2 * tid + k;
+                uint32_t at = S.r.ib.tot[h];
+#pragma unroll
+                for (int w = 0; w < kSHalf; w++) {
+                    const uint32_t c = c16[w * kSBuckets + h];
+                    c16[w * kSBuckets + h] = (uint16_t)at;
+                    at += c;
+                }
+            }
+            __syncthreads();
         }
+        if (first_half == (half == 0)) {
+#pragma unroll 1
+            for (int r = 0; r < 16; r++) {   // in order: a wave's entries enter each bucket ascending
+                const int i = wave * 1024 + r * 64 + lane;
+                if (i < nidx) {
+                    const uint32_t x = a0 + (uint32_t)(i * kSStride);
+                    const uint32_t h = shash(lds4(S, x), ldsb(S, x + 4));
+                    const uint32_t old = atomicAdd(&S.r.ib.cnt[hw * (kSBuckets / 2) + (h >> 1)],
+                                                   (h & 1u) ? 0x10000u : 1u);
+                    const uint32_t slot = (old >> ((h & 1u) * 16)) & 0xFFFFu;
+#ifdef APE_SEG_GUARD
+                    if (slot >= (uint32_t)nidx) atomicOr(&S.wmax[15], 1u << 5);
+#endif
+                    S.u.ix.pos[slot] = (uint16_t)(i * kSStride);
+                }
+            }
+        }
+        __syncthreads();
     }
-    __syncthreads();
 
 #ifdef APE_SEG_GUARD
     {   // diagnostic: index consistency (bits of the block's result)
         int bad = 0;
-        const uint32_t o0 = S.u.ix.offs[tid], o1 = S.u.ix.offs[tid + 1];
-        if (o1 < o0) atomicOr(&S.wmax[15], 1u << 1);
         if (tid == 0 && S.u.ix.offs[kSBuckets] != (uint32_t)nidx) atomicOr(&S.wmax[15], 1u << 2);
-        for (uint32_t k = o0 + 1; k < o1 && k < (uint32_t)kSIdx; k++)
-            bad += S.u.ix.pos[k] <= S.u.ix.pos[k - 1];
+        for (int hh = tid; hh < kSBuckets; hh += kSThreads) {
+            const uint32_t o0 = S.u.ix.offs[hh], o1 = S.u.ix.offs[hh + 1];
+            if (o1 < o0) atomicOr(&S.wmax[15], 1u << 1);
+            for (uint32_t k = o0 + 1; k < o1 && k < (uint32_t)kSIdx; k++)
+                bad += S.u.ix.pos[k] <= S.u.ix.pos[k - 1];
+            for (uint32_t k = o0; k < o1 && k < (uint32_t)kSIdx; k++)
+                if (shash(lds4(S, a0 + S.u.ix.pos[k]), ldsb(S, a0 + S.u.ix.pos[k] + 4)) != (uint32_t)hh) { atomicOr(&S.wmax[15], 1u << 4); break; }
+        }
         if (bad) atomicOr(&S.wmax[15], 1u << 3);
-        for (uint32_t k = o0; k < o1 && k < (uint32_t)kSIdx; k++)
-            if (shash(lds4(S, a0 + S.u.ix.pos[k]), ldsb(S, a0 + S.u.ix.pos[k] + 4)) != (uint32_t)tid) { atomicOr(&S.wmax[15], 1u << 4); break; }
         __syncthreads();
         if (S.wmax[15]) g_trip = 100 + (int)S.wmax[15];
         __syncthreads();
     }
 #endif
-    // ---- PARSE: lane tid, segment [s0, s1) ----
-    const int s0 = tid * kSSeg;
+    STAT(1);
+#ifdef APE_SEG_INDEXONLY   // diagnostic: load + index alone
+    if (tid == 0) a.result[b] = 1;
+    return;
+#endif
+    // ---- PARSE: 16-byte segments, handed out to the lanes of each wave as they finish ----
+    // Wave w owns segments [256w, 256w + 256) (4 KiB of the block); a lane whose segment is
+    // done takes the next one (lanes ranked by lane id: deterministic), so the lanes of a wave
+    // finish together instead of waiting for the longest of 64 fixed segments.
     const int mfl = n - 12;                  // matches start at <= n-12 (:585)
-    int nrec = 0;
-    if (s0 < n) {
-        const int s1 = s0 + kSSeg < n ? s0 + kSSeg : n;
-        // matches end at <= n-12 (not n-5): a match cut to start where the previous
-        // segment's coverage ends then still starts at <= n-12
-        const int capE = s1 + kSCapX < mfl ? s1 + kSCapX : mfl;
-        int q = s0 > 1 ? s0 : 1, anchor = s0;
-        int gp = 0;
-        while (q < s1 && q <= mfl && nrec < kSRec) {
-            SGUARD(gp, 200, 1)
-            const uint4 own = lds16(S, a0 + (uint32_t)q);
-            const uint32_t h = shash(own.x, own.y);
-            int lo = (int)S.u.ix.offs[h], hi = (int)S.u.ix.offs[h + 1];
-            const int blo = lo;
-            int gb = 0;
-            while (lo < hi) {   // first entry >= q
-                SGUARD(gb, 40, 2)
-                const int mid = (lo + hi) >> 1;
-                if ((int)S.u.ix.pos[mid] < q) lo = mid + 1;
-                else hi = mid;
+    for (int i = tid; i < kSRecS * kSSegs; i += kSThreads) S.r.rec[i] = 0u;   // empty slots
+    __syncthreads();
+#ifdef APE_LZ4_STATS
+    uint32_t c_probe = 0, c_bs = 0, c_ext = 0, c_cu = 0;
+#define SCOUNT(v) (v)++
+#else
+#define SCOUNT(v)
+#endif
+    {
+        const float inv_span = 1.0f / (float)(nidx * kSStride > 0 ? nidx * kSStride : 1);
+        int seg = lane, nxt = 64;            // wave-local segment; next one to hand out
+        int gs = 0, s1 = 0, capE = 0, q = 0, anchor = 0, nrec = 0;
+        auto start_seg = [&]() {
+            gs = wave * kSWaveSegs + seg;
+            const int s0 = gs * kSSeg;
+            if (seg >= kSWaveSegs || s0 >= n || s0 > mfl) {
+                seg = kSWaveSegs;   // nothing left for this lane
+                return;
             }
-            const int room = capE - q;
-            int best = 0, bestc = 0;
+            s1 = s0 + kSSeg < n ? s0 + kSSeg : n;
+            // matches end at <= n-12 (not n-5): a match cut to start where the coverage of
+            // the segments before ends then still starts at <= n-12
+            capE = s1 + kSCapX < mfl ? s1 + kSCapX : mfl;
+            q = s0 > 1 ? s0 : 1;
+            anchor = s0;
+            nrec = 0;
+        };
+        start_seg();
+        int gp = 0;
+        for (;;) {
+            const bool act = seg < kSWaveSegs;
+            if (!wave_any(act)) break;
+            if (act) {
+                SGUARD(gp, 4096, 1)
+                SCOUNT(c_probe);
+                const uint4 own = lds16(S, a0 + (uint32_t)q);
+                const uint32_t h = shash(own.x, own.y);
+                const int blo = (int)S.u.ix.offs[h], bhi = (int)S.u.ix.offs[h + 1];
+                // The bucket lists its positions in ascending order, spread about evenly over
+                // the block: read the 8 entries around where q falls (one LDS read) and find
+                // the first >= q among them.  When they do not bracket q: binary search (rare).
+                const int est = blo + (int)((float)(bhi - blo) * ((float)q * inv_span));
+                int w0 = est - 5 < bhi - 8 ? est - 5 : bhi - 8;
+                w0 = w0 > blo ? w0 : blo;
+                const l32x4a2 Wv = *(const l32x4a2 *)&S.u.ix.pos[w0];
+                const int nv = bhi - w0;   // window entries inside the bucket
+                uint32_t e8[8];
 #pragma unroll
-            for (int d = 0; d < kSDepth; d++) {
-                const int j = lo - 1 - d;
-                const int c = j >= blo ? (int)S.u.ix.pos[j] : q;
-                if (c < q) {
+                for (int i = 0; i < 8; i++) {
+                    const uint32_t dw = i < 2 ? Wv.x : i < 4 ? Wv.y : i < 6 ? Wv.z : Wv.w;
+                    e8[i] = i < nv ? ((dw >> ((i & 1) * 16)) & 0xFFFFu) : 0x10000u;
+                }
+                // ascending: k = entries < q by three compares
+                int k = e8[3] < (uint32_t)q ? 4 : 0;
+                {
+                    const uint32_t v1 = k ? e8[5] : e8[1];
+                    k += v1 < (uint32_t)q ? 2 : 0;
+                    const uint32_t v0 = k == 0 ? e8[0] : k == 2 ? e8[2] : k == 4 ? e8[4] : e8[6];
+                    k += v0 < (uint32_t)q ? 1 : 0;
+                    if (k == 7 && e8[7] < (uint32_t)q) k = 8;
+                }
+                uint64_t r4;   // entries lb-4 .. lb-1 (lb = w0 + k), 16 bits each, lb-1 on top
+                int lb = w0 + k, wlo = w0;   // entries below wlo are not in r4
+                if ((k == 0 && w0 > blo) || (k == 8 && w0 + 8 < bhi)) {
+                    int lo = blo, hi = bhi;
+                    int gb = 0;
+                    while (lo < hi) {   // first entry >= q
+                        SGUARD(gb, 40, 2)
+                        SCOUNT(c_bs);
+                        const int mid = (lo + hi) >> 1;
+                        if ((int)S.u.ix.pos[mid] < q) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    lb = lo;
+                    wlo = blo;
+                    r4 = 0;
+#pragma unroll
+                    for (int d = 0; d < 4; d++)
+                        if (lb - 4 + d >= blo) r4 |= (uint64_t)S.u.ix.pos[lb - 4 + d] << (16 * d);
+                } else {
+                    const uint64_t lo64 = ((uint64_t)Wv.y << 32) | Wv.x, hi64 = ((uint64_t)Wv.w << 32) | Wv.z;
+                    const int sh = (k - 4) * 16;
+                    r4 = sh >= 64 ? hi64 : sh > 0 ? (lo64 >> sh) | (hi64 << (64 - sh)) : sh == 0 ? lo64 : lo64 << (-sh);
+                }
+                const int room = capE - q;
+                int best = 0, bestc = 0;
+#ifdef APE_SEG_PICK8   // measured: -3.5 % kernel time for ratio 3.39 -> 3.19 (not kept)
+                // the four latest candidates, prefiltered on 8 bytes: the first (latest) that
+                // matches 8 bytes, else the first that matches 4, is measured over 16 bytes
+                int cpick = 0, lvl = 0;   // lvl: 2 = 8 bytes equal, 1 = 4 bytes
+#pragma unroll
+                for (int d = kSDepth - 1; d >= 0; d--) {   // latest last: it wins ties
+                    const int j = lb - 1 - d;
+                    const int c = (int)((r4 >> (48 - 16 * d)) & 0xFFFFu);
+                    const l32x2 v = *(const l32x2 *)((const uint8_t *)S.blk + a0 + (uint32_t)c);
+                    const int lv = (j >= wlo && c < q && v.x == own.x) ? (v.y == own.y ? 2 : 1) : 0;
+                    if (lv > 0 && lv >= lvl) { lvl = lv; cpick = c; }
+                }
+                if (lvl && room >= kMinMatch) {
+                    int l = (int)prefix16(own, lds16(S, a0 + (uint32_t)cpick));
+                    best = l < room ? l : room;
+                    bestc = cpick;
+                }
+#else
+                // the four latest candidates; those whose first 4 bytes match are measured,
+                // one at a time per lane (a loop as long as the lane with the most of them)
+                int cd[kSDepth];
+                uint32_t okm = 0;
+#pragma unroll
+                for (int d = 0; d < kSDepth; d++) {
+                    const int j = lb - 1 - d;
+                    cd[d] = (int)((r4 >> (48 - 16 * d)) & 0xFFFFu);
+                    if (j >= wlo && cd[d] < q && lds4(S, a0 + (uint32_t)cd[d]) == own.x) okm |= 1u << d;
+                }
+                if (room < kMinMatch) okm = 0;
+                while (okm) {
+                    const uint32_t d = (uint32_t)__builtin_ctz(okm);
+                    okm &= okm - 1u;
+                    const int c = d == 0 ? cd[0] : d == 1 ? cd[1] : d == 2 ? cd[2] : cd[3];
                     int l = (int)prefix16(own, lds16(S, a0 + (uint32_t)c));
                     l = l < room ? l : room;
                     if (l > best) { best = l; bestc = c; }
                 }
-            }
-            if (best < kMinMatch) { q++; continue; }
-            int len = best;
-            if (best == 16) {
-                int ge = 0;
-                while (len < room) {
-                    SGUARD(ge, 40, 3)
-                    const int l = (int)prefix16(lds16(S, a0 + (uint32_t)(q + len)),
-                                                lds16(S, a0 + (uint32_t)(bestc + len)));
-                    len += l;
-                    if (l < 16) break;
+#endif
+                if (best < kMinMatch) {
+                    q++;
+                } else {
+                    int len = best;
+                    if (best == 16) {
+                        int ge = 0;
+                        while (len < room) {
+                            SGUARD(ge, 40, 3)
+                            SCOUNT(c_ext);
+                            const int l = (int)prefix16(lds16(S, a0 + (uint32_t)(q + len)),
+                                                        lds16(S, a0 + (uint32_t)(bestc + len)));
+                            len += l;
+                            if (l < 16) break;
+                        }
+                        len = len < room ? len : room;
+                    }
+                    int m = q, c = bestc;   // catch-up (:623-627): up to 4 bytes, one compare
+                    {
+                        SCOUNT(c_cu);
+                        const int room_b = (m - anchor) < c ? (m - anchor) : c;
+                        const uint32_t x = lds4(S, a0 + (uint32_t)(m - 4)) ^ lds4(S, a0 + (uint32_t)(c - 4));
+                        const int eq = x ? (int)(__builtin_clz(x) >> 3) : 4;   // equal bytes just before
+                        const int t = room_b <= 0 ? 0 : (eq < room_b ? eq : room_b);
+                        m -= t;
+                        c -= t;
+                        len += t;
+                    }
+                    S.r.rec[nrec * kSSegs + gs] = (uint32_t)(m - gs * kSSeg) | ((uint32_t)len << 4) | ((uint32_t)(m - c) << 16);
+                    nrec++;
+                    anchor = m + len;
+                    q = anchor;
                 }
-                len = len < room ? len : room;
             }
-            int m = q, c = bestc;   // catch-up (:623-627)
-            int gc = 0;
-            while (m > anchor && c > 0 && ldsb(S, a0 + (uint32_t)(m - 1)) == ldsb(S, a0 + (uint32_t)(c - 1))) {
-                SGUARD(gc, 80, 4)
-                m--;
-                c--;
-                len++;
+            const bool done = act && (q >= s1 || q > mfl || nrec >= kSRecS);
+            const uint64_t D = wave_ballot(done);
+            if (done) {
+                seg = nxt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(D >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)D, 0u));
+                start_seg();
             }
-            S.r.rec[nrec * kSThreads + tid] = (uint32_t)(m - s0) | ((uint32_t)len << 6) | ((uint32_t)(m - c) << 16);
-            nrec++;
-            anchor = m + len;
-            q = anchor;
+            nxt += __popcll(D);
         }
     }
-
-    // ---- SPLICE: where each segment's kept sequences start; sizes; output offsets ----
-    // Coverage after segment k: C_k = f_k(C_{k-1}), f_k(c) = c + 4 <= e_k ? e_k : c with e_k
-    // the end of k's last match (a match cut to start at c is kept only if >= 4 bytes; all
-    // of k's earlier matches end before its last one starts).  Scanned as keys e << 10 | k of
-    // the segments that produce coverage (0 for the others), so that the exclusive prefix max
-    // also names the producer.  C is the fixed point of key = excl-prefix-max(f(key)), reached
-    // from the plain prefix max of e in one or two rounds (a cut < 4 bytes is rare); a
-    // sequential pass settles the rest.
-    uint32_t elast = 0;
-    if (nrec > 0) {
-        const uint32_t r = S.r.rec[(nrec - 1) * kSThreads + tid];
-        elast = (uint32_t)s0 + (r & 63u) + ((r >> 6) & 1023u);
+    STAT(2);
+#ifdef APE_LZ4_STATS
+    {   // wave-max and lane-sum of the loop counts, for wave 0
+        const uint32_t mp = lane_val(wave_incl_max(c_probe), 63), mb = lane_val(wave_incl_max(c_bs), 63);
+        const uint32_t me = lane_val(wave_incl_max(c_ext), 63), mc = lane_val(wave_incl_max(c_cu), 63);
+        const uint32_t sp = lane_val(wave_incl_sum(c_probe), 63);
+        STAT_ADD(11, mp);
+        STAT_ADD(12, mb);
+        STAT_ADD(13, me);
+        STAT_ADD(14, mc);
+        STAT_ADD(15, sp);
     }
-    const uint32_t key0 = nrec > 0 ? (elast << 10) | (uint32_t)tid : 0u;
+#endif
+
+#ifdef APE_SEG_PARSEONLY   // diagnostic: instruction counts of load + index + parse alone
+    if (tid == 0) a.result[b] = 1;
+    return;
+#endif
+    // ---- SPLICE: thread t owns the 64-byte region of segments 4t .. 4t+3 ----
+    // Its records, in order, are walked against the coverage C that the regions before it
+    // leave: a match ending inside C is dropped, one that straddles it is cut (kept if >= 4
+    // bytes), and a kept match that starts exactly where the previous one ends, at its offset,
+    // continues it (one match re-found by the next 16-byte segment).  The region's walk is a
+    // function f_t(C) of the incoming coverage; C_t = f_t(C_{t-1}) is scanned as keys
+    // C << 10 | t of the regions that produce coverage (0 for the others), so that the
+    // exclusive prefix max also names the producer: the fixed point of
+    // key = excl-prefix-max(f(key)), reached from the plain prefix max of the regions' last
+    // match ends in one or two rounds (a cut < 4 bytes is rare); a sequential pass settles
+    // the rest.
+    const int s0 = tid * 64;   // this thread's region
+    auto rec_at = [&](int i) -> uint32_t {   // i-th slot of the region: segment i / 3, slot i % 3
+        return S.r.rec[(i % kSRecS) * kSSegs + tid * 4 + i / kSRecS];
+    };
+    auto region_f = [&](uint32_t c) -> uint32_t {   // coverage after the region, entering with c
+        uint32_t pe = c;
+#pragma unroll 1
+        for (int i = 0; i < 4 * kSRecS; i++) {
+            const uint32_t w = rec_at(i);
+            if (!w) continue;
+            const uint32_t m = (uint32_t)s0 + (uint32_t)(i / kSRecS) * kSSeg + (w & 15u), e = m + ((w >> 4) & 4095u);
+            if (e <= pe) continue;
+            if (m < pe && e - pe < (uint32_t)kMinMatch) continue;
+            pe = e;
+        }
+        return pe;
+    };
+    uint32_t elast = 0;
+#pragma unroll 1
+    for (int i = 0; i < 4 * kSRecS; i++) {
+        const uint32_t w = rec_at(i);
+        if (w) {
+            const uint32_t e = (uint32_t)s0 + (uint32_t)(i / kSRecS) * kSSeg + (w & 15u) + ((w >> 4) & 4095u);
+            elast = e > elast ? e : elast;
+        }
+    }
+    const uint32_t key0 = elast ? (elast << 10) | (uint32_t)tid : 0u;
     uint32_t allk;
     uint32_t ck = block_excl_max(S, key0, wave, lane, &allk);
+    STAT(3);
     for (int it = 0;; it++) {
-        const uint32_t E = (ck >> 10) + 4u <= elast ? key0 : 0u;
+        const uint32_t cin = ck >> 10, cout = region_f(cin);
+        const uint32_t E = cout > cin ? (cout << 10) | (uint32_t)tid : 0u;
         uint32_t all2;
         const uint32_t c2 = block_excl_max(S, E, wave, lane, &all2);
         const bool moved = c2 != ck;
         ck = c2;
         allk = all2;
         if (!__syncthreads_or(moved)) break;
-        if (it == 3) {   // sequential: thread 0 walks the segments (ends in LDS)
-            uint32_t *ends = (uint32_t *)S.u.stage;
-            ends[tid] = elast;
-            __syncthreads();
-            if (tid == 0) {
-                uint32_t c = 0, kk = 0;
-                for (int k = 0; k < kSThreads; k++) {
-                    const uint32_t e = ends[k];
-                    ends[k] = kk;
-                    if ((kk >> 10) + 4u <= e) kk = (e << 10) | (uint32_t)k;
-                    c = kk;
+        if (it == 3) {   // sequential: thread 0 walks the regions (their outgoing coverage
+                         // depends on the incoming one: each thread tabulates nothing; so
+                         // thread 0 asks each region in turn through LDS)
+            uint32_t *cv = (uint32_t *)S.u.stage;   // cv[t] = incoming key of region t
+            if (tid == 0) cv[0] = 0u;
+            for (int t2 = 0; t2 < kSThreads; t2++) {
+                __syncthreads();
+                if (tid == t2) {
+                    const uint32_t ci = cv[t2] >> 10, co = region_f(ci);
+                    if (t2 + 1 < kSThreads) cv[t2 + 1] = co > ci ? (co << 10) | (uint32_t)t2 : cv[t2];
+                    else S.wmax[0] = co > ci ? (co << 10) | (uint32_t)t2 : cv[t2];
                 }
-                S.wmax[0] = c;
             }
             __syncthreads();
-            ck = ends[tid];
+            ck = cv[tid];
             allk = S.wmax[0];
             __syncthreads();
             break;
@@ -390,35 +634,53 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
     }
     const uint32_t cover = ck >> 10, cover_all = allk >> 10;
 
-    // Runs longer than a segment: a kept match that starts exactly where the coverage ends,
-    // at the offset of the match that ends there, continues that match (every 64 bytes of a
-    // long run are found again by the next segment).  It is folded into its head sequence:
-    // T_k = val_k + (pass_k ? T_{k+1} : 0) sums the continuations after segment k (val = the
-    // continuing length, pass = the segment holds nothing else, so the chain goes on), a
-    // segmented suffix scan; the head (a segment's last kept match) takes T_{k+1} on top.
-    uint32_t kc = 0, f_m = 0, f_len = 0, f_off = 0, l_off = 0;
-    {
-        uint32_t pe = cover;
+    // The region's kept sequences, local continuations folded: fn(lit_start, m, len, off, k)
+    // for the k-th sequence (k = 1, 2, ...); returns the count.
+    auto walk = [&](auto fn) -> uint32_t {
+        uint32_t pe = cover, cnt = 0, pm = 0, plen = 0, poff = 0, plit = 0;
+        bool have = false;
 #pragma unroll 1
-        for (int r = 0; r < nrec; r++) {
-            const uint32_t w = S.r.rec[r * kSThreads + tid];
-            uint32_t m = (uint32_t)s0 + (w & 63u), len = (w >> 6) & 1023u;
-            const uint32_t e = m + len;
+        for (int i = 0; i < 4 * kSRecS; i++) {
+            const uint32_t w = rec_at(i);
+            if (!w) continue;
+            uint32_t m = (uint32_t)s0 + (uint32_t)(i / kSRecS) * kSSeg + (w & 15u), len = (w >> 4) & 4095u;
+            const uint32_t off = w >> 16, e = m + len;
             if (e <= pe) continue;
             if (m < pe) {
+                if (e - pe < (uint32_t)kMinMatch) continue;
                 len = e - pe;
                 m = pe;
-                if (len < (uint32_t)kMinMatch) continue;
             }
-            if (kc == 0) { f_m = m; f_len = len; f_off = w >> 16; }
-            l_off = w >> 16;
-            kc++;
+            if (have && m == pm + plen && off == poff) {
+                plen += len;   // the same match, re-found by the next segment
+            } else {
+                if (have) fn(plit, pm, plen, poff, ++cnt);
+                plit = pe;
+                pm = m;
+                plen = len;
+                poff = off;
+                have = true;
+            }
             pe = e;
         }
-    }
+        if (have) fn(plit, pm, plen, poff, ++cnt);
+        return cnt;
+    };
+
+    // Runs longer than a region: a region's first kept sequence that starts exactly where the
+    // coverage ends, at the offset of the sequence that ends there, continues that sequence.
+    // It is folded into its head: T_t = val_t + (pass_t ? T_{t+1} : 0) sums the continuations
+    // after region t (val = the continuing length, pass = the region holds nothing else, so
+    // the chain goes on), a segmented suffix scan; the head (a region's last kept sequence)
+    // takes T_{t+1} on top.
+    uint32_t f_m = 0, f_len = 0, f_off = 0, l_off = 0;
+    const uint32_t kc = walk([&](uint32_t, uint32_t m, uint32_t len, uint32_t off, uint32_t k) {
+        if (k == 1) { f_m = m; f_len = len; f_off = off; }
+        l_off = off;
+    });
     uint32_t *segoff = (uint32_t *)S.u.stage;            // [1024] last kept offset
     uint32_t *segvp = segoff + kSThreads;                 // [1024] val | !pass << 31
-    uint32_t *segT = segvp + kSThreads;                   // [1025] T_k
+    uint32_t *segT = segvp + kSThreads;                   // [1025] T_t
     segoff[tid] = l_off;
     __syncthreads();
     const bool cont = kc > 0 && ck != 0u && f_m == cover && f_off == segoff[ck & 1023u];
@@ -427,7 +689,7 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
     segvp[tid] = val | (pass ? 0u : 0x80000000u);
     if (tid == 0) segT[kSThreads] = 0u;
     __syncthreads();
-    {   // thread t scans segment 1023 - t: S_t = x_t + (reset_t ? 0 : S_{t-1})
+    {   // thread t scans region 1023 - t: S_t = x_t + (reset_t ? 0 : S_{t-1})
         const uint32_t vp = segvp[kSThreads - 1 - tid];
         uint32_t x = vp & 0x7FFFFFFFu, fl = vp >> 31;
 #pragma unroll
@@ -438,8 +700,8 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
                 fl |= pf;
             }
         }
-        // carry across waves: wave w's lanes without a reset before them take the previous
-        // waves' running value (sequential over the 16 wave totals in LDS)
+        // carry across waves: lanes without a reset before them take the previous waves'
+        // running value (sequential over the 16 wave totals in LDS)
         if (lane == 63) {
             S.wsum[wave] = x;
             S.wmax[wave] = fl;
@@ -451,37 +713,23 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
         segT[kSThreads - 1 - tid] = x;
         __syncthreads();
     }
-    const uint32_t tail = segT[tid + 1];   // T_{k+1}
+    const uint32_t tail = segT[tid + 1];   // T_{t+1}
     uint32_t sz = 0;
-    {
-        uint32_t pe = cover, k = 0;
-#pragma unroll 1
-        for (int r = 0; r < nrec; r++) {
-            const uint32_t w = S.r.rec[r * kSThreads + tid];
-            uint32_t m = (uint32_t)s0 + (w & 63u), len = (w >> 6) & 1023u;
-            const uint32_t e = m + len;
-            if (e <= pe) continue;
-            if (m < pe) {
-                len = e - pe;
-                m = pe;
-                if (len < (uint32_t)kMinMatch) continue;
-            }
-            k++;
-            if (!(k == 1 && cont)) {   // a continuation's bytes are its head's
-                const uint32_t L = len + (k == kc ? tail : 0u);
-                const int lit = (int)(m - pe);
-                sz += 1u + (uint32_t)extlen(lit) + (uint32_t)lit + 2u + (uint32_t)extlen((int)L - 4);
-            }
-            pe = e;
-        }
-    }
+    walk([&](uint32_t lit0, uint32_t m, uint32_t len, uint32_t, uint32_t k) {
+        if (k == 1 && cont) return;   // a continuation's bytes are its head's
+        const uint32_t L = len + (k == kc ? tail : 0u);
+        const int lit = (int)(m - lit0);
+        sz += 1u + (uint32_t)extlen(lit) + (uint32_t)lit + 2u + (uint32_t)extlen((int)L - 4);
+    });
     __syncthreads();   // segT / segvp (stage area) read before the emission writes it
+    STAT(4);
     uint32_t body;
     const uint32_t obase = block_excl_sum(S, sz, wave, lane, &body);
     const int lastrun = n - (int)cover_all;
     const uint32_t total = body + 1u + (uint32_t)extlen(lastrun) + (uint32_t)lastrun;
     const uint32_t litonly = 1u + (uint32_t)extlen(n) + (uint32_t)n;
 
+    STAT(5);
     if (total >= litonly) {
         // ---- incompressible: one literal run (what the reference emits for such input) ----
         if (litonly > (uint32_t)cap) {
@@ -501,53 +749,42 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
         return;
     }
 
+#ifdef APE_SEG_NOEMIT   // diagnostic: everything but the emission
+    if (tid == 0) a.result[b] = (int)total;
+    return;
+#endif
     // ---- EMIT: staging windows of kSStage bytes ----
 #pragma unroll 1
     for (uint32_t w0 = 0; w0 < total; w0 += (uint32_t)kSStage) {
         __syncthreads();   // the index (first window) / the previous window's store is done
         uint32_t lsrc = 0, ldst = 0, llen = 0;   // this lane's long literal run, if any
         {
-            uint32_t pe = cover, o = obase, k = 0;
-#pragma unroll 1
-            for (int r = 0; r < nrec; r++) {
-                const uint32_t w = S.r.rec[r * kSThreads + tid];
-                uint32_t m = (uint32_t)s0 + (w & 63u), len = (w >> 6) & 1023u;
-                const uint32_t off = w >> 16, e = m + len;
-                if (e <= pe) continue;
-                if (m < pe) {
-                    len = e - pe;
-                    m = pe;
-                    if (len < (uint32_t)kMinMatch) continue;
-                }
-                k++;
-                if (k == 1 && cont) {   // continuation: written with its head
-                    pe = e;
-                    continue;
-                }
+            uint32_t o = obase;
+            walk([&](uint32_t lit0, uint32_t m, uint32_t len, uint32_t off, uint32_t k) {
+                if (k == 1 && cont) return;   // continuation: written with its head
                 if (k == kc) len += tail;
-                const int lit = (int)(m - pe), ml = (int)len - 4;
+                const int lit = (int)(m - lit0), ml = (int)len - 4;
                 put(S, o++, w0, ((uint32_t)(lit < 15 ? lit : 15) << 4) | (uint32_t)(ml < 15 ? ml : 15));
                 if (lit >= 15) o = put_len(S, o, w0, lit);
                 if (lit > kSLongRun) {
-                    lsrc = pe;
+                    lsrc = lit0;
                     ldst = o;
                     llen = (uint32_t)lit;
                 } else {
 #pragma unroll 1
-                    for (int i = 0; i < lit; i++) put(S, o + (uint32_t)i, w0, ldsb(S, a0 + pe + (uint32_t)i));
+                    for (int i = 0; i < lit; i++) put(S, o + (uint32_t)i, w0, ldsb(S, a0 + lit0 + (uint32_t)i));
                 }
                 o += (uint32_t)lit;
                 put(S, o++, w0, off & 255u);
                 put(S, o++, w0, off >> 8);
                 if (ml >= 15) o = put_len(S, o, w0, ml);
-                pe = e;
-            }
+            });
             if (tid == kSThreads - 1) {   // the last literals (:732-751)
                 uint32_t o2 = body;
                 put(S, o2++, w0, (uint32_t)(lastrun < 15 ? lastrun : 15) << 4);
                 if (lastrun >= 15) o2 = put_len(S, o2, w0, lastrun);
                 // (a long last run is copied by the wave in the second pass below: a lane
-                // has at most one long run among its own records, the first kept one's)
+                // has at most one long run among its own sequences, the first one's)
                 if (lastrun <= kSLongRun)
 #pragma unroll 1
                     for (int i = 0; i < lastrun; i++) put(S, o2 + (uint32_t)i, w0, ldsb(S, a0 + cover_all + (uint32_t)i));
@@ -591,6 +828,9 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
             for (uint32_t i = (uint32_t)tid; i < wl; i += kSThreads) d[i] = S.u.stage[i];
         }
     }
+    STAT(6);
+    STAT_ADD(10, 1);
+    STATS_FLUSH(g_seg_stats);
 #ifdef APE_SEG_GUARD
     if (g_trip) a.result[b] = -1000000 - g_trip * 1000 - (tid & 1023) * 0;
     else

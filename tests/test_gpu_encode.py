@@ -103,7 +103,7 @@ def test_benchmark_blocks_ratio_and_roundtrip(cuda, product, oracle):
     gpu_ratio = 64 * 65536 / sum(rs[:64])
     ref_ratio = 64 * 65536 / sum(ref[:64])
     print("64 KiB compressible ratio: gpu %.4f reference %.4f" % (gpu_ratio, ref_ratio))
-    assert gpu_ratio >= 0.97 * ref_ratio
+    assert gpu_ratio >= 0.99 * ref_ratio   # a 2 % regression must fail
     assert rs[64:128] == [4114] * 64  # incompressible: one literal run, as the reference
     # and the GPU decoder restores them too
     from test_gpu_decode import run_decode
@@ -221,7 +221,9 @@ def test_acceleration(cuda, product, oracle):
     print("ratio by acceleration", {a: round(r, 4) for a, r in ratio.items()},
           "reference", {a: round(r, 4) for a, r in ref.items()})
     assert ratio[1] >= ratio[2] > ratio[4] > ratio[8] > ratio[1 << 30]
-    assert ratio[2] >= 0.9 * ratio[1]
+    # acceleration 1 is compress_default: the segment encoder (four candidates per position)
+    # compresses better than the reference's single-candidate search
+    assert ratio[1] >= ref[1]
     for a in (2, 4, 8):
         assert abs(ratio[a] / ref[a] - 1.0) <= ACCEL_RATIO_TOL, (a, ratio[a], ref[a])
     # a huge acceleration probes only the three positions after each match end (and the

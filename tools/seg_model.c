@@ -170,10 +170,24 @@ int main(int argc, char **argv)
     uint8_t *in = malloc((size_t)n * nb);
     int *prev = malloc(sizeof(int) * n), *head = malloc(sizeof(int) * (1 << 24));
     seq_t *seqs = malloc(sizeof(seq_t) * n);
-    synth_blocks(in, n, n, 0, nb, kind);
+    synth_blocks(in, n, n, 0, nb, kind == 2 ? 0 : kind);
+    if (kind == 2) {   /* random bytes + back-copies of 11..86 bytes (tests' _boundary_copies) */
+        static const int lens[] = {11, 12, 13, 15, 16, 17, 19, 20, 21, 75, 76, 77, 79, 80, 81, 83, 84, 85, 86};
+        uint64_t r = 88172645463325252ULL;
+        for (int b = 0; b < nb; b++) {
+            uint8_t *o = in + (size_t)b * n;
+            int i = 2048;
+            while (i < n) {
+                r ^= r << 13; r ^= r >> 7; r ^= r << 17;
+                int ln = lens[r % 19], off = 1 + (int)((r >> 8) % (uint64_t)(i < 65535 ? i - 1 : 65534));
+                for (int k = 0; k < ln && i < n; k++, i++) o[i] = o[i - off];
+                if (i < n) o[i++] = (uint8_t)(r >> 40);
+            }
+        }
+    }
     struct { int hlog, stride, depth, nseg, ways, cap, meas; } cfg[] = {
-        {12, 4, 4, 1024, 0, 64, 16}, {11, 4, 4, 1024, 0, 64, 16}, {10, 4, 4, 1024, 0, 64, 16},
-        {10, 4, 4, 1024, 0, 64, 8}, {10, 4, 2, 1024, 0, 64, 16}, {11, 4, 4, 512, 0, 64, 16}, {10, 2, 4, 1024, 0, 64, 16}};
+        {11, 4, 4, 1024, 0, 64, 16}, {11, 4, 4, 4096, 0, 64, 16}, {11, 4, 3, 4096, 0, 64, 16},
+        {11, 4, 2, 4096, 0, 64, 16}, {11, 4, 4, 2048, 0, 64, 16}};
     struct { int hlog, stride, depth, nseg; } cfg_old[] = {
         {13, 1, 1, 64}, {13, 1, 2, 64}, {13, 1, 4, 64}, {13, 2, 1, 64}, {13, 4, 1, 64},
         {13, 4, 2, 64}, {14, 1, 1, 64}, {14, 1, 2, 64}, {14, 2, 2, 64}, {14, 4, 2, 64},
