@@ -872,6 +872,50 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
         return;
     }
 
+    // One literal run holding the whole block (incompressible input, e.g. SURVEY config 2):
+    // the reference reads the token and its length bytes (:1329-1342), then takes the final-
+    // literals branch (:1346-1366): ret = the run if it ends exactly at csize and fits cap,
+    // else -(ip)-1.  Here the length bytes are scanned 64 at a time and the run is copied
+    // global -> global, 16 bytes per lane, without the LDS staging or the output window.
+    if (!PARTIAL && !FASTD && !DICT && D.csize >= 32 && D.cap > 0 && D.src[0] >= 0xF0u) {
+        // bytes 1.. while 255 and ip < csize - 15 after the read (:1334-1337): J = the last
+        // one read; all before it are 255
+        int J = 0;
+        for (int base = 1;; base += 64) {
+            const int i = base + lane;
+            const uint32_t byte = D.src[i < D.csize ? i : D.csize - 1];   // (never past src)
+            const bool stop = i + 1 >= D.csize - 15 || byte != 255u;
+            const uint64_t m = wave_ballot(stop);
+            if (m) {
+                J = base + __builtin_ctzll(m);
+                break;
+            }
+        }
+        const long long L = 15ll + 255ll * (J - 1) + (long long)D.src[J];
+        if ((long long)J + 1 + L == (long long)D.csize) {
+            if (L > (long long)D.cap) {
+                if (lane == 0) a.result[b] = -(J + 1) - 1;
+                return;
+            }
+            gcu8 *s = D.src + J + 1;
+            gu8 *d = D.dst;
+            const int n16 = (int)(L >> 4);
+            int k = lane;
+            for (; k + 192 < n16; k += 256) {   // four 16-byte loads in flight per lane
+                const uint4 v0 = gload16(s + 16 * k), v1 = gload16(s + 16 * (k + 64));
+                const uint4 v2 = gload16(s + 16 * (k + 128)), v3 = gload16(s + 16 * (k + 192));
+                gstore16(d + 16 * k, v0);
+                gstore16(d + 16 * (k + 64), v1);
+                gstore16(d + 16 * (k + 128), v2);
+                gstore16(d + 16 * (k + 192), v3);
+            }
+            for (; k < n16; k += 64) gstore16(d + 16 * k, gload16(s + 16 * k));
+            for (int i = 16 * n16 + lane; i < (int)L; i += 64) d[i] = s[i];
+            if (lane == 0) a.result[b] = (int)L;
+            return;
+        }
+    }
+
     STATS_DECL
     int P = 0;               // next token (wave-uniform)
     uint32_t op = 0;         // its output position
