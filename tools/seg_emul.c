@@ -12,7 +12,7 @@
 
 void synth_blocks(uint8_t *out, int n, long long stride, long long first, int nb, int kind);
 
-enum { THREADS = 1024, SEG = 64, STRIDE = 4, HLOG = 10, NB = 1 << HLOG, CAPX = 64, NREC = 14,
+enum { THREADS = 1024, SEG = 64, STRIDE = 4, HLOG = 11, NB = 1 << HLOG, CAPX = 64, NREC = 13,
        DEPTH = 4 };
 
 static uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
