@@ -69,6 +69,15 @@ int APE_LZ4_compress_fast_batch_dev(const char *const *d_src, const int *d_srcSi
                                     char *const *d_dst, const int *d_dstCap, int *d_result,
                                     int nblocks, int acceleration, void *stream);
 
+/* Greedy-exact mode (slow, for debugging): == N x APE_LZ4_compress_fast
+ * (ref src/ape_lz4.c:789-808 -> LZ4_compress_generic :530-755, byU16), BYTE FOR BYTE -- the
+ * reference's sequential parse run by one wave per block, limitedOutput's early exits (0)
+ * included; acceleration <= 1 is compress_default.  Deviation: a negative d_dstCap[i] gives 0
+ * (the reference treats it as a huge unsigned capacity in its last-literals check). */
+int APE_LZ4_compress_exact_batch_dev(const char *const *d_src, const int *d_srcSize,
+                                     char *const *d_dst, const int *d_dstCap, int *d_result,
+                                     int nblocks, int acceleration, void *stream);
+
 /* d_result[i] <- decoded size, or -(consumed)-1, as APE_LZ4_decompress_safe. */
 int APE_LZ4_decompress_safe_batch_dev(const char *const *d_src, const int *d_compressedSize,
                                       char *const *d_dst, const int *d_maxDecompressedSize,

@@ -18,7 +18,7 @@ __all__ = [
     "decompress_safe", "decompress_safe_partial", "compress_batch", "decompress_batch",
     "decompress_partial_batch", "synth_blocks", "gpu_init", "gpu_last_error", "GpuError",
     "MAX_BLOCK", "ERANGE", "frame_offsets", "frame_pack", "decompress_frames",
-    "compress_prefix_batch", "decompress_dict_batch", "compress_fast_ptr_batch",
+    "compress_prefix_batch", "decompress_dict_batch", "compress_fast_ptr_batch", "compress_exact_ptr_batch",
     "decompress_fast_ptr_batch", "compress_destSize_ptr_batch", "RxBuf",
     "compress_destSize_scratch_ptr_batch", "destSize_scratch_size",
     "socket_send_blocks", "socket_recv_blocks", "socket_stats", "set_oneshot_host_below",
@@ -64,6 +64,7 @@ def lib():
             "APE_LZ4_gpu_set_oneshot_host_below": (i, [i]),
             "APE_LZ4_compress_batch_dev": (i, [p, p, p, p, p, i, p]),
             "APE_LZ4_compress_fast_batch_dev": (i, [p, p, p, p, p, i, i, p]),
+            "APE_LZ4_compress_exact_batch_dev": (i, [p, p, p, p, p, i, i, p]),
             "APE_LZ4_compress_destSize_batch_dev": (i, [p, p, p, p, p, i, p]),
             "APE_LZ4_compress_destSize_scratch_size": (sz, [i]),
             "APE_LZ4_compress_destSize_batch_scratch_dev": (i, [p, p, p, p, p, i, p, sz, p]),
@@ -225,6 +226,16 @@ def compress_fast_ptr_batch(src_ptrs, src_sizes, dst_ptrs, caps, results, accele
     _check(lib().APE_LZ4_compress_fast_batch_dev(
         _ptr(src_ptrs), _ptr(src_sizes), _ptr(dst_ptrs), _ptr(caps), _ptr(results), n,
         acceleration, _stream(stream)), "APE_LZ4_compress_fast_batch_dev")
+
+
+def compress_exact_ptr_batch(src_ptrs, src_sizes, dst_ptrs, caps, results, acceleration=1,
+                             stream=None):
+    """Greedy-exact mode: N x APE_LZ4_compress_fast byte for byte (the reference's own
+    sequential parse, one wave per block; slow, for debugging)."""
+    n = src_sizes.shape[0]
+    _check(lib().APE_LZ4_compress_exact_batch_dev(
+        _ptr(src_ptrs), _ptr(src_sizes), _ptr(dst_ptrs), _ptr(caps), _ptr(results), n,
+        acceleration, _stream(stream)), "APE_LZ4_compress_exact_batch_dev")
 
 
 def compress_destSize_ptr_batch(src_ptrs, src_sizes, dst_ptrs, targets, results, stream=None):

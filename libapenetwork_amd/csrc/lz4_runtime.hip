@@ -297,6 +297,18 @@ int APE_LZ4_compress_fast_batch_dev(const char *const *d_src, const int *d_srcSi
     return finish_launch(launch_encode(a, (hipStream_t)stream), "lz4_encode_kernel");
 }
 
+int APE_LZ4_compress_exact_batch_dev(const char *const *d_src, const int *d_srcSize,
+                                     char *const *d_dst, const int *d_dstCap, int *d_result,
+                                     int nblocks, int acceleration, void *stream) {
+    if (nblocks < 0 || (nblocks > 0 && (!d_src || !d_srcSize || !d_dst || !d_dstCap || !d_result)))
+        return APE_LZ4_GPU_EINVAL;
+    int rc = check_device();
+    if (rc) return rc;
+    BlockArgs a = ptr_args(d_src, d_srcSize, d_dst, d_dstCap, nullptr, d_result, nblocks);
+    a.accel = acceleration;
+    return finish_launch(launch_encode_exact(a, (hipStream_t)stream), "lz4_encode_exact_kernel");
+}
+
 int APE_LZ4_decompress_safe_batch_dev(const char *const *d_src, const int *d_compressedSize,
                                       char *const *d_dst, const int *d_maxDecompressedSize,
                                       int *d_result, int nblocks, void *stream) {
