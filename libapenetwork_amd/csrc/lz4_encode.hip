@@ -61,10 +61,6 @@ hipError_t enc_stats_read(unsigned long long *out, int reset) {
 
 namespace {
 
-#ifdef APE_EXP_CNT_NTR   // diagnostic: counters only, no phase timers
-#undef STAT
-#define STAT(i) do {} while (0)
-#endif
 
 #ifndef APE_LZ4_HLOG
 #define APE_LZ4_HLOG 13
@@ -108,10 +104,7 @@ constexpr uint32_t kGroups = 16;
 #define APE_LZ4_ERING 1024
 #endif
 constexpr uint32_t kRingE = APE_LZ4_ERING;  // recent input bytes (own, stage 2, end-2, literals)
-// Diagnostic A/B: with a 64 KiB ring the whole block window sits in LDS
-// and the candidate bytes (Y, E) are read from it instead of global memory -- 84 KiB
-// of LDS per block, one block per CU.  Never the product.
-constexpr bool kWin = kRingE >= 65536u;
+static_assert(kRingE < 65536u, "the ring holds recent input, not the block's window (DESIGN.md 3.1.1)");
 #ifndef APE_LZ4_SCRBITS
 #define APE_LZ4_SCRBITS 6
 #endif
@@ -180,35 +173,6 @@ __device__ __forceinline__ void vm_wait() {
     static_assert(N >= 0 && N < 16, "vmcnt");
     __builtin_amdgcn_s_waitcnt(N | (7 << 4) | (15 << 8));
 }
-
-// Diagnostic (sensitivity A/B only, never the product): N dependent-free 4-cycle VALU ops
-// (APE_EXP_PAD_P / _W / _E / _PL: producer, walker, emitter VALU; producer LDS reads).
-template <int N>
-__device__ __forceinline__ void pad_valu(uint32_t &x) {
-#pragma unroll
-    for (int i = 0; i < N; i++) asm volatile("v_mul_u32_u24 %0, %0, 3" : "+v"(x));
-}
-template <int N>
-__device__ __forceinline__ void pad_lds(uint32_t &x) {
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-        uint32_t y;
-        asm volatile("ds_read_b32 %0, %1 offset:16384" : "=v"(y) : "v"(x & 0x3FCu));
-        asm volatile("s_waitcnt lgkmcnt(0)\n v_add_u32 %0, %0, %1" : "+v"(x) : "v"(y));
-    }
-}
-#ifndef APE_EXP_PAD_P
-#define APE_EXP_PAD_P 0
-#endif
-#ifndef APE_EXP_PAD_W
-#define APE_EXP_PAD_W 0
-#endif
-#ifndef APE_EXP_PAD_PL
-#define APE_EXP_PAD_PL 0
-#endif
-#ifndef APE_EXP_PAD_E
-#define APE_EXP_PAD_E 0
-#endif
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -372,21 +336,9 @@ __device__ __forceinline__ void put_len(gu8 *o, uint32_t v) {
 
 // 16 / 8 input bytes at x from the ring (the mirrored tail keeps a read that starts in
 // the last 64 bytes contiguous): aligned dword reads + v_alignbyte.  (Measured against
-// single unaligned ds_read_b128 / _b64, APE_EXP_UNALIGNED_RING: 12.5 vs 11.3 ms per 16384
+// single unaligned ds_read_b128 / _b64 (round 4): 12.5 vs 11.3 ms per 16384
 // blocks -- fewer VALU instructions, but a 1-byte lane stride makes the unaligned reads
 // slow.)
-#ifdef APE_EXP_UNALIGNED_RING
-typedef uint32_t l32x4 __attribute__((ext_vector_type(4), aligned(1)));
-typedef uint32_t l32x2 __attribute__((ext_vector_type(2), aligned(1)));
-__device__ __forceinline__ uint4 ring16(const EncLds &S, uint32_t x) {
-    const l32x4 v = *(const l32x4 *)((const uint8_t *)S.ring + (x & (kRingE - 1)));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ uint2 ring8(const EncLds &S, uint32_t x) {
-    const l32x2 v = *(const l32x2 *)((const uint8_t *)S.ring + (x & (kRingE - 1)));
-    return make_uint2(v.x, v.y);
-}
-#else
 __device__ __forceinline__ uint4 ring16(const EncLds &S, uint32_t x) {
     const uint32_t *r = S.ring + ((x >> 2) & (kRingE / 4 - 1));
     const uint32_t sh = x & 3u;
@@ -400,7 +352,6 @@ __device__ __forceinline__ uint2 ring8(const EncLds &S, uint32_t x) {
     const uint32_t w0 = r[0], w1 = r[1], w2 = r[2];
     return make_uint2(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh));
 }
-#endif
 
 // NW dwords in[pos, pos + 4 NW) (NW = 4 or 6).  fast: the window lies inside [0, n)
 // (vector loads); otherwise byte loads, bytes outside [0, n) read as 0 (the edge steps
@@ -536,7 +487,7 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
         wave_sync();
         if (hashable) S.scr[hs] = 0xFFFFFFFFu;
     }
-    if (!kWin) prod_fetch_t<SMALL, FAST>(B, k, lane, cT, Y);
+    prod_fetch_t<SMALL, FAST>(B, k, lane, cT, Y);
 }
 
 // R(k): ring copy of chunk k (own bytes for C1 and stage 2, match_end - 2, literals; zero
@@ -556,11 +507,6 @@ __device__ __forceinline__ void prod_ring(EncLds &S, const Blk &B, int k, int la
 // own bytes in[p-4, p+20) of chunk k from the ring (ring tail = 0 before 0)
 __device__ __forceinline__ void prod_own(const EncLds &S, int k, int lane, uint32_t (&X)[6]) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-#ifdef APE_EXP_UNALIGNED_RING
-    const uint4 a = ring16(S, p - 4u);
-    const uint2 b = ring8(S, p + 12u);
-    X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w; X[4] = b.x; X[5] = b.y;
-#else
     // 7 aligned dwords, 6 alignbytes
     const uint32_t *r = S.ring + (((p - 4u) >> 2) & (kRingE / 4 - 1));
     const uint32_t sh = p & 3u;
@@ -569,7 +515,6 @@ __device__ __forceinline__ void prod_own(const EncLds &S, int k, int lane, uint3
     for (int t = 0; t < 7; t++) W[t] = r[t];
 #pragma unroll
     for (int t = 0; t < 6; t++) X[t] = __builtin_amdgcn_alignbyte(W[t + 1], W[t], sh);
-#endif
 }
 
 // Stage-2 group of this lane for the truncated lanes of ranks [first, first + kGroups):
@@ -620,15 +565,6 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
                                              const uint32_t (&X)[6], const uint32_t (&Y)[6],
                                              uint32_t cT, uint32_t jL, uint32_t h, Part &R) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
-    uint32_t Yw[6];
-    if (kWin) {   // candidate bytes from the LDS window (chunks <= k+1 are in it by now)
-        const bool tryT = k < B.nch && cT < p && cT >= 4u;
-        const uint4 a = ring16(S, tryT ? cT - 4u : 0u);
-        const uint2 b = ring8(S, tryT ? cT + 12u : 16u);
-        Yw[0] = a.x; Yw[1] = a.y; Yw[2] = a.z; Yw[3] = a.w; Yw[4] = b.x; Yw[5] = b.y;
-    }
-    const uint32_t (&Yr)[6] = kWin ? Yw : Y;
-#define Y Yr
     // FAST (chunk k + 1 lies inside the block with 83 bytes to spare, k >= 1): every lane is
     // live, hashable and may start a match
     const bool live = FAST || k < B.nch;
@@ -687,7 +623,6 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
 #endif
     R.bk = umin(back4(X[0], pickL ? Z[0] : Y[0]), R.c);  // c - back >= 0
     R.iy = ((okT | okL) ? p - R.c : 0u) | (h << 16);
-#undef Y
 }
 
 // S2(k), at the start of the second half (off C1's latency chain, next to C2(k-1)):
@@ -701,11 +636,6 @@ __device__ __forceinline__ void prod_stage2_issue(const EncLds &S, const Blk &B,
     R.rank = lane_rank(tb);
     uint32_t cb;
     const bool ga = stage2_group(R, lane, 0u, p, cb, R.eo);
-    if (kWin) {
-        const uint4 e = ring16(S, ga ? cb : 0u);
-        E[0] = e.x; E[1] = e.y; E[2] = e.z; E[3] = e.w;
-        return;
-    }
     // cb + 16 <= c + base + kExt2 < p + 80 (c < p)
     loadv<4>(B.in, B.un, ga ? cb : 0u, E, FAST || (!SMALL && 64 * k + 148 <= B.n));
 }
@@ -722,12 +652,7 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
         for (uint32_t first = kGroups; first < R.ntr; first += kGroups) {   // rare
             uint32_t cb, eo, E2[4];
             const bool ga = stage2_group(R, lane, first, p, cb, eo);
-            if (kWin) {
-                const uint4 e = ring16(S, ga ? cb : 0u);
-                E2[0] = e.x; E2[1] = e.y; E2[2] = e.z; E2[3] = e.w;
-            } else {
-                loadv<4>(B.in, B.un, ga ? cb : 0u, E2, FAST || (!SMALL && 64 * k + 148 <= B.n));
-            }
+            loadv<4>(B.in, B.un, ga ? cb : 0u, E2, FAST || (!SMALL && 64 * k + 148 <= B.n));
             const uint32_t m2 = bperm(stage2_len(S, lane, eo, E2), 4u * (R.rank - first));
             if (R.rank - first < kGroups) mine = m2;
         }
@@ -1271,7 +1196,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             // step -- and with it the waits -- is the same on every path.
             // In flight, oldest first: A(s+2), Y(s+1), A(s+3), E(s) -> A(s+2) at 3 (APF; without:
             // A(s+2), Y(s+1), E(s)).
-            vm_wait<kWin ? 0 : 3>();
+            vm_wait<3>();
             STAT(9);   // (stats build: load waits)
             // ring copy of chunk s+2 (loaded a step ago), then C1(s+1)'s own bytes (chunks
             // s+1 and s+2) from the ring: one wave's LDS operations complete in order.  (Until
@@ -1293,33 +1218,17 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             // Y(s+1) x2, E(s), A(s+3), Y(s+2) x2 -> Y(s+1) at 4
 #endif
             STAT(5);
-            vm_wait<kWin ? 1 : 4>();
+            vm_wait<4>();
             STAT(9);
             prod_measure<SMALL, F>(S, B, s + 1, lane, X6, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q);
-            if (APE_EXP_PAD_P) { uint32_t x = (uint32_t)lane; pad_valu<APE_EXP_PAD_P>(x); (void)x; }
-            if (APE_EXP_PAD_PL) { uint32_t x = (uint32_t)lane; pad_lds<APE_EXP_PAD_PL>(x); (void)x; }
             STAT(5);
             __syncthreads();
             STAT(6);
             prod_stage2_issue<SMALL, F>(S, B, s + 1, lane, nxt.q, nxt.E);
-#ifdef APE_EXP_CNT_NTR
-            if (s + 1 < B.nch) {   // diagnostic: stage-2 queue sizes and same-offset runs
-                const uint32_t ntr = nxt.q.ntr;
-                const uint32_t off = 64u * (uint32_t)(s + 1) + (uint32_t)lane - nxt.q.c;
-                const uint32_t offn = bperm(off, (uint32_t)lane + 1u);
-                const uint64_t tm = nxt.q.tmask;
-                const bool tn = lane < 63 && ((tm >> (lane + 1)) & 1ull);
-                const uint64_t der = wave_ballot(lane_in(tm) && tn && offn == off);
-                const uint32_t roots = ntr - (uint32_t)__popcll(der);
-                STAT_ADD(0, ntr); STAT_ADD(1, ntr > 16u); STAT_ADD(2, ntr > 32u); STAT_ADD(3, ntr > 48u);
-                STAT_ADD(4, 1); STAT_ADD(5, roots); STAT_ADD(6, roots > 16u); STAT_ADD(7, roots > 32u);
-                STAT_ADD(8, roots > 8u); STAT_ADD(9, (uint32_t)__popcll(nxt.q.smask)); // (= roots)
-            }
-#endif
             // E(s), A(s+3), Y(s+2) x2, E(s+1) -> E(s) at 4 (A(s+3), issued half a step ago,
             // is not needed before the next step)
             STAT(7);
-            vm_wait<kWin ? 0 : (APE_LZ4_APF ? 3 : 4)>();   // (APF: Y(s+2), A(s+4), E(s+1) after E(s))
+            vm_wait<(APE_LZ4_APF ? 3 : 4)>();   // (APF: Y(s+2), A(s+4), E(s+1) after E(s))
             STAT(9);
             prod_finish<SMALL, F>(S, B, s, lane, cur.q, cur.E);
             STAT(7);
@@ -1376,28 +1285,18 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         // chunk s - 1 is walked during step s for s in [k0 + 1, nch]; the first step and
         // the steps past the last chunk only keep the barrier count (separate loops, so
         // the walking loop carries no per-step predicate)
-#ifdef APE_EXP_NOWALK
-        const int s2 = k0 + 1;   // diagnostic: instruction count without the walker
-#else
         const int s2 = nch + 1;
-#endif
         __syncthreads();   // step k0
         __syncthreads();
         int s = k0 + 1;
         for (; s < s2; s++) {
             walk_chain<ACC>(S, B, s - 1, lane, W, O);
-            if (APE_EXP_PAD_W) { uint32_t x = (uint32_t)lane; pad_valu<APE_EXP_PAD_W>(x); (void)x; }
             STAT(0);
             __syncthreads();
             STAT(4);
             walk_finish<ACC>(B, s - 1, lane, W, O);
             walk_publish(S, B, s - 1, lane, O, qn);
-#ifndef APE_EXP_CNT_NTR
             STAT_ADD(11, __popcll(O.members));
-#else   // members the walker extends (their match reached C1 + stage 2's measured length)
-            STAT_ADD(11, __popcll(O.members & wave_ballot((O.iv.x & I_TRUNC) != 0u)));
-            STAT_ADD(12, __popcll(O.members));
-#endif
             STAT(1);
             STAT_ADD(10, 3);
             __syncthreads();
@@ -1425,14 +1324,6 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
     E.bigm = 0;
     E.r = E.lit = E.mlm4 = E.off = E.ba = 0;
     __syncthreads();
-#ifdef APE_EXP_NOEMIT   // diagnostic: instruction count without the emitter (no output)
-    for (int s = k0; s < nsteps; s++) {
-        __syncthreads();
-        __syncthreads();
-    }
-    if (lane == 0) *result = 0;
-    return;
-#endif
     for (int s = k0; s < nsteps; s++) {
         // S.qn: the walker's count as of its last publish (before the previous barrier)
         const uint32_t avail = (uint32_t)__builtin_amdgcn_readfirstlane(S.qn) - E.qc;
@@ -1449,7 +1340,6 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         } else {
             emit_step(S, B, lane, E);
         }
-        if (APE_EXP_PAD_E) { uint32_t x = (uint32_t)lane; pad_valu<APE_EXP_PAD_E>(x); (void)x; }
         STAT(2);
         __syncthreads();
         STAT(14);
@@ -1529,11 +1419,7 @@ lz4_encode_kernel(BlockArgs a) {
     B.nr = (uint32_t)nr;
     B.k0 = D / 64;
     // compress_fast's acceleration (:789-808): the reference's probe pattern (walk_chain)
-#ifdef APE_EXP_NOL
-    B.noL = true;   // diagnostic: no in-chunk candidate search (its LDS atomics)
-#else
     B.noL = ACC && !APE_LZ4_ACC_L;
-#endif
     B.stride = ACC ? (a.accel < (1 << 20) ? (uint32_t)a.accel : 1u << 20) : 1u;
     B.cap = (uint32_t)icap;
     B.un = (uint32_t)B.n;

@@ -158,8 +158,10 @@ __device__ __forceinline__ int extlen(int v) { return v >= 15 ? (v - 15) / 255 +
 // iteration bound; a tripped bound ends the loop and marks the block's result.
 #ifdef APE_SEG_GUARD
 #define SGUARD(cnt, lim, code) if (++(cnt) > (lim)) { g_trip = (code); break; }
+#define SGUARD_DECL(cnt) int cnt = 0;
 #else
 #define SGUARD(cnt, lim, code)
+#define SGUARD_DECL(cnt)
 #endif
 
 // block-wide exclusive sum over the 1024 threads; *total = the sum of all
@@ -406,7 +408,7 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
             nrec = 0;
         };
         start_seg();
-        int gp = 0;
+        SGUARD_DECL(gp)
         for (;;) {
             const bool act = seg < kSWaveSegs;
             if (!wave_any(act)) break;
@@ -443,7 +445,7 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
                 int lb = w0 + k, wlo = w0;   // entries below wlo are not in r4
                 if ((k == 0 && w0 > blo) || (k == 8 && w0 + 8 < bhi)) {
                     int lo = blo, hi = bhi;
-                    int gb = 0;
+                    SGUARD_DECL(gb)
                     while (lo < hi) {   // first entry >= q
                         SGUARD(gb, 40, 2)
                         SCOUNT(c_bs);
@@ -507,7 +509,7 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
                 } else {
                     int len = best;
                     if (best == 16) {
-                        int ge = 0;
+                        SGUARD_DECL(ge)
                         while (len < room) {
                             SGUARD(ge, 40, 3)
                             SCOUNT(c_ext);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build an encoder-only diagnostic variant: lz4_encode.hip with extra -D flags, linked with
 # the product's other objects -> libapenetwork_amd/libape_lz4_amd_<name>.so (never the product).
-# usage: bash tools/enc_variant.sh NAME "-DAPE_EXP_..." [encoder source]
+# usage: bash tools/enc_variant.sh NAME "-DAPE_LZ4_..." [encoder source]
 set -e
 cd "$(dirname "$0")/.."
 V=$1; DEFS=$2; SRC=${3:-libapenetwork_amd/csrc/lz4_encode.hip}
