@@ -61,7 +61,6 @@ namespace {
 constexpr int kSThreads = 1024, kSWaves = kSThreads / 64, kSHalf = kSWaves / 2;
 constexpr int kSSeg = 16;                         // bytes per segment (a lane's unit of work)
 constexpr int kSSegs = kMaxBlock / kSSeg;         // 4096 segments
-constexpr int kSWaveSegs = kSSegs / kSWaves;      // 256 segments (4 KiB) per wave
 constexpr int kSRecS = 3;                         // record slots per segment
 constexpr int kSStride = 4;                       // indexed positions: multiples of 4
 constexpr int kSHLog = 11, kSBuckets = 1 << kSHLog;
@@ -93,6 +92,7 @@ struct SegLds {
     } r;
     uint32_t wsum[kSWaves];
     uint32_t wmax[kSWaves];
+    uint32_t segnext;                             // parse: next segment to hand out
 };
 constexpr int kSStage = (int)sizeof(((SegLds *)0)->u.stage) & ~15;
 static_assert(sizeof(SegLds) <= 160 * 1024, "LDS");
@@ -375,12 +375,14 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
     if (tid == 0) a.result[b] = 1;
     return;
 #endif
-    // ---- PARSE: 16-byte segments, handed out to the lanes of each wave as they finish ----
-    // Wave w owns segments [256w, 256w + 256) (4 KiB of the block); a lane whose segment is
-    // done takes the next one (lanes ranked by lane id: deterministic), so the lanes of a wave
-    // finish together instead of waiting for the longest of 64 fixed segments.
+    // ---- PARSE: 16-byte segments, handed out to the lanes as they finish ----
+    // Thread t starts with segment t; a lane whose segment is done takes the next one from a
+    // block-wide counter (one LDS atomic per wave and round), so the waves finish together
+    // instead of waiting for the wave with the slowest 4 KiB.  A segment's records depend only
+    // on its bytes and the index, not on the lane that parses it: the output is deterministic.
     const int mfl = n - 12;                  // matches start at <= n-12 (:585)
     for (int i = tid; i < kSRecS * kSSegs; i += kSThreads) S.r.rec[i] = 0u;   // empty slots
+    if (tid == 0) S.segnext = (uint32_t)kSThreads;
     __syncthreads();
 #ifdef APE_LZ4_STATS
     uint32_t c_probe = 0, c_bs = 0, c_ext = 0, c_cu = 0;
@@ -390,13 +392,13 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
 #endif
     {
         const float inv_span = 1.0f / (float)(nidx * kSStride > 0 ? nidx * kSStride : 1);
-        int seg = lane, nxt = 64;            // wave-local segment; next one to hand out
+        int seg = tid;                       // block segment
         int gs = 0, s1 = 0, capE = 0, q = 0, anchor = 0, nrec = 0;
         auto start_seg = [&]() {
-            gs = wave * kSWaveSegs + seg;
+            gs = seg;
             const int s0 = gs * kSSeg;
-            if (seg >= kSWaveSegs || s0 >= n || s0 > mfl) {
-                seg = kSWaveSegs;   // nothing left for this lane
+            if (seg >= kSSegs || s0 >= n || s0 > mfl) {
+                seg = kSSegs;   // nothing left for this lane
                 return;
             }
             s1 = s0 + kSSeg < n ? s0 + kSSeg : n;
@@ -410,7 +412,7 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
         start_seg();
         SGUARD_DECL(gp)
         for (;;) {
-            const bool act = seg < kSWaveSegs;
+            const bool act = seg < kSSegs;
             if (!wave_any(act)) break;
             if (act) {
                 SGUARD(gp, 4096, 1)
@@ -539,11 +541,16 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
             }
             const bool done = act && (q >= s1 || q > mfl || nrec >= kSRecS);
             const uint64_t D = wave_ballot(done);
-            if (done) {
-                seg = nxt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(D >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)D, 0u));
-                start_seg();
+            if (D) {
+                const int f = __builtin_ctzll(D);
+                uint32_t nb0 = 0;
+                if (lane == f) nb0 = atomicAdd(&S.segnext, (uint32_t)__popcll(D));
+                nb0 = lane_val(nb0, f);
+                if (done) {
+                    seg = (int)nb0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(D >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)D, 0u));
+                    start_seg();
+                }
             }
-            nxt += __popcll(D);
         }
     }
     STAT(2);
