@@ -269,7 +269,8 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t idx) {
 }
 
 // The sequence that would start at window position rel (token at P + rel), parsed
-// speculatively from the staged bytes: token, literal length, offset, one match-length
+// speculatively from the staged bytes: token, one literal-length extension byte (the
+// reference's loop :1331-1342 reads exactly one when it is < 255), offset, one match-length
 // extension byte, and where the next token would be.
 struct Spec {
     uint32_t lit, off, ml;
@@ -284,16 +285,19 @@ template <bool FASTD>
 __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, uint32_t rel) {
     Spec z;
     const uint32_t r = (uint32_t)(P - D.s0) + rel;
-    const uint32_t tok = L.stage[r];
-    const uint32_t lit = tok >> 4, mn = tok & 15u;
-    const uint32_t r1 = r + 1u + lit;           // offset bytes (then the ml byte)
+    // token and the byte after it as two byte reads (one unaligned ds_read_u16 per lane, at a
+    // 1-byte lane stride, measured +7.8 % decode time; an aligned 8-byte read + funnel ties)
+    const uint32_t tok = L.stage[r], e1 = L.stage[r + 1u];
+    const bool litx = tok >= 0xF0u;             // literal length 15 + e1
+    const uint32_t lit = litx ? 15u + e1 : tok >> 4, mn = tok & 15u;
+    const uint32_t r1 = r + 1u + (litx ? 1u : 0u) + lit;   // offset bytes (then the ml byte)
     const uint32_t a1 = r1 & ~3u;
     const l32x2 w = *(const l32x2 *)&L.stage[a1];   // one ds_read_b64 (any byte address)
     const uint32_t x = funnel(w.y, w.x, r1 & 3u);
     const uint32_t e = (x >> 16) & 0xFFu;
     z.lit = lit;
     z.off = x & 0xFFFFu;
-    z.ipl = P + (int)rel + 1;
+    z.ipl = P + (int)rel + 1 + (litx ? 1 : 0);
     z.ipo = z.ipl + (int)lit + 2;
     const bool mlx = mn == 15u;
     z.mlx = mlx;
@@ -304,7 +308,10 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
     z.mlover = (int)r1 > lim - 2 - kLastLiterals;                  // ipo + 5 > csize
     z.mlerr = !FASTD && mlx && z.mlover;
     z.r1 = r1;
-    z.cx = lit == 15u || (mlx && e == 255u && !z.mlerr);
+    // complex (the scalar restatement): a literal length with more than one extension byte,
+    // a long literal run whose offset bytes lie past the staged input, or a match length with
+    // more than one extension byte
+    z.cx = (litx && (e1 == 255u || r1 + 3u > (uint32_t)kStage)) || (mlx && e == 255u && !z.mlerr);
     z.ml = mlx ? 15u + e : mn;
     z.q = z.ipo + (mlx ? 1 : 0);
     return z;
@@ -317,7 +324,8 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
 // sequence (a window holds <= 22: each sequence takes >= 3 input bytes).  cnt members
 // (lanes [0, cnt)); X = the chain's exit (next token position >= 64, or kHopTerm after a
 // final / failing sequence, kHopCplx before a complex token); lastp = the last member.
-constexpr uint32_t kHopTerm = 0x80u, kHopCplx = 0xC0u;
+// A real hop is < 0x200 (63 + 1 + 1 + 269 + 2 + 1); the codes are above it.
+constexpr uint32_t kHopTerm = 0x200u, kHopCplx = 0x300u;
 template <bool FASTD>
 __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, uint32_t &pos,
                                          int &cnt, uint32_t &X, uint32_t &lastp) {
@@ -326,9 +334,9 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
     uint32_t hop;
     {
         // the hop alone: mlerr implies fin_in (ipo + 5 = ipl + lit + 7), and the successor
-        // relative to P is lane + lit + 3 (+1 with the ml byte)
+        // relative to P is the staged position after the literals + 2 (+1 with the ml byte)
         const Spec z = spec_at<FASTD>(L, D, P, (uint32_t)D.lane);
-        const uint32_t qr = (uint32_t)D.lane + z.lit + (z.mlx ? 4u : 3u);
+        const uint32_t qr = z.r1 - (uint32_t)(P - D.s0) + (z.mlx ? 3u : 2u);
         hop = 4u * (z.cx ? kHopCplx : (z.fin_in ? kHopTerm : qr));
     }
     // Exits absorb as a max: a real hop moves forward (J[a] > a), and an exit (>= 256) reads
@@ -383,11 +391,11 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     int cntA;
     chain_at<FASTD>(L, D, P, posA, cntA, XA, lastA);
     const bool cplxA = XA == kHopCplx;
-    // the complex token is not a member.  (XA is wave-uniform and is 64..84, kHopTerm 0x80 or
-    // kHopCplx 0xC0: bits 7 and 6 both set only for kHopCplx -- scalar arithmetic, where a
-    // select on the bool was materialised in a VGPR)
-    static_assert(kHopCplx == 0xC0u && kHopTerm == 0x80u, "hop exit codes");
-    const int nmA = cntA - (int)((XA >> 7) & (XA >> 6) & 1u);
+    // the complex token is not a member.  (XA is wave-uniform and is 64..0x1FF, kHopTerm
+    // 0x200 or kHopCplx 0x300: bits 9 and 8 both set only for kHopCplx -- scalar arithmetic,
+    // where a select on the bool was materialised in a VGPR)
+    static_assert(kHopCplx == 0x300u && kHopTerm == 0x200u, "hop exit codes");
+    const int nmA = cntA - (int)((XA >> 9) & (XA >> 8) & 1u);
     const int PB = P + (int)XA;
     const bool two = XA < kHopTerm && PB - D.s0 + kWinNeed <= kStage;
     int nmB = 0, nmC = 0, Pn, PC = PB;
@@ -396,7 +404,7 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
         uint32_t XB, lastB;
         int cntB;
         chain_at<FASTD>(L, D, PB, posB, cntB, XB, lastB);
-        nmB = cntB - (int)((XB >> 7) & (XB >> 6) & 1u);   // (as nmA)
+        nmB = cntB - (int)((XB >> 9) & (XB >> 8) & 1u);   // (as nmA)
         PC = PB + (int)XB;
         // a third window while the members still fit the wave (<= 41 + 22 lanes) and the
         // descriptors the array (nd + nm <= kMaxDesc), and its bytes are staged
@@ -407,7 +415,7 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
             int cntC;
             chain_at<FASTD>(L, D, PC, posC, cntC, XC, lastC);
             cplx = XC == kHopCplx;
-            nmC = cntC - (int)((XC >> 7) & (XC >> 6) & 1u);
+            nmC = cntC - (int)((XC >> 9) & (XC >> 8) & 1u);
             Pn = PC + (int)(XC >= kHopTerm ? lastC : XC);
         } else {
             cplx = XB == kHopCplx;
@@ -439,7 +447,7 @@ __device__ int parse_window(WaveLds &L, const Dec &D, int &P, uint32_t &op, int 
     const uint32_t opl = op + ex;
     // The checks of :1345-1447 in the reference's order, as selects (no divergent
     // branches).  32-bit unsigned arithmetic is exact here: cap, csize > 0, a window
-    // token has lit < 15 and ml < 274, and op + ex stays far below 2^32.
+    // token has lit < 270 and ml < 274, and op + ex stays far below 2^32.
     const uint32_t cpy = opl + lit, ucap = (uint32_t)D.cap;
     const uint32_t iend = (uint32_t)ipl + lit;  // input position after the literals
     // FASTD (:1346-1366 with endOnOutputSize): final once the literals pass cap - 8,
