@@ -638,6 +638,68 @@ __device__ __forceinline__ void lane_match(WaveLds &L, const Dec &D, uint32_t ba
     }
 }
 
+// Round 1 in two halves: the sources are read (window or dst history / dictionary) before the
+// segment's literals are written, and stored after them, so the history loads' latency overlaps
+// the literal copies.  (A round-1 source lies before the segment: no literal overwrites it.)
+// Measured -1.1 % decode time (131072 blocks, medians of 9).
+struct MLoad {
+    uint4 v0, v1, v2, v3;
+};
+template <bool DICT>
+__device__ __forceinline__ void lane_match_load(WaveLds &L, const Dec &D, uint32_t base, bool go,
+                                                uint32_t ma, uint32_t n, uint32_t off, bool glb,
+                                                MLoad &u) {
+    if (!go || (off != 0u && off < n)) return;   // (self-overlap: all in the store half)
+    const int ps = (int)ma - (int)off;
+    const uint32_t t1 = umin(16u, n - 16u), t2 = umin(32u, n - 16u), t3 = n - 16u;
+    const bool u1 = n > 16u, u2 = n > 32u, u3 = n > 48u;
+    if (!glb) {
+        const uint8_t *s = L.win + ((uint32_t)ps - base);
+        u.v0 = lds16(s);
+        if (u1) u.v1 = lds16(s + t1);
+        if (u2) u.v2 = lds16(s + t2);
+        if (u3) u.v3 = lds16(s + t3);
+    } else if (!DICT) {
+        gcu8 *d = (gcu8 *)D.dst;
+        const uint32_t o0 = (uint32_t)ps;
+        u.v0 = gload16_nt(d + o0);
+        if (u1) u.v1 = gload16_nt(d + (o0 + t1));
+        if (u2) u.v2 = gload16_nt(d + (o0 + t2));
+        if (u3) u.v3 = gload16_nt(d + (o0 + t3));
+    } else {
+        gcu8 *s = ps < 0 ? D.dend + ps : (gcu8 *)D.dst + ps;
+        u.v0 = gload16_nt(s);
+        if (u1) u.v1 = gload16_nt(s + t1);
+        if (u2) u.v2 = gload16_nt(s + t2);
+        if (u3) u.v3 = gload16_nt(s + t3);
+    }
+}
+__device__ __forceinline__ void lane_match_store(WaveLds &L, uint32_t base, bool go, uint32_t ma,
+                                                 uint32_t n, uint32_t off, MLoad &u) {
+    if (!go) return;
+    uint8_t *w = L.win + (ma - base);
+    const int ps = (int)ma - (int)off;
+    const uint32_t t1 = umin(16u, n - 16u), t2 = umin(32u, n - 16u), t3 = n - 16u;
+    const bool u1 = n > 16u, u2 = n > 32u, u3 = n > 48u;
+    if (off != 0u && off < n) {   // overlaps itself (off >= 16, n > 16): unit after unit
+        const uint8_t *s = L.win + ((uint32_t)ps - base);
+        lds_st16(w, lds16(s));
+        if (u1) lds_st16(w + t1, lds16(s + t1));
+        if (u2) lds_st16(w + t2, lds16(s + t2));
+        if (u3) lds_st16(w + t3, lds16(s + t3));
+        return;
+    }
+    if (off == 0u) u.v0 = u.v1 = u.v2 = u.v3 = make_uint4(0, 0, 0, 0);
+    if (n >= 16u) {
+        lds_st16(w, u.v0);
+        if (u1) lds_st16(w + t1, u.v1);
+        if (u2) lds_st16(w + t2, u.v2);
+        if (u3) lds_st16(w + t3, u.v3);
+    } else {
+        lds_put_small<true>(w, u.v0, n);
+    }
+}
+
 // Per-lane sequence of the batch: literal [o, m) from input ls, match [m, me) at offset off.
 struct Seq {
     uint32_t o, m, me, ls, off;
@@ -689,6 +751,9 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
     const bool glb = lane_in(~off0m & ~inwm);
     const int pe = lane_in(off0m) ? -0x7FFFFFFF : (lane_in(ovlm) ? (int)ma : pe0);
     const uint64_t mpm = wave_ballot(nm != 0u);
+    const uint64_t r1m = mpm & lpm & wave_ballot(pe <= (int)S0);
+    MLoad r1u;
+    lane_match_load<DICT>(L, D, base, lane_in(r1m), ma, nm, off, glb, r1u);
 
     // literals
     for (uint64_t lc = nlm & ~litm; lc; lc &= lc - 1ull) {
@@ -703,8 +768,7 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
         else lds_put_small<false>(w, v, nl);
     }
     // round 1
-    const uint64_t r1m = mpm & lpm & wave_ballot(pe <= (int)S0);
-    lane_match<DICT>(L, D, base, lane_in(r1m), ma, nm, off, glb);
+    lane_match_store(L, base, lane_in(r1m), ma, nm, off, r1u);
     uint64_t pm = mpm & ~r1m;
     if (!pm) return;
     // sequences owning [max(ps, S0), pe): k0 = owner(first byte), k1 = owner(last byte),
