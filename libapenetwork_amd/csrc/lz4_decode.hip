@@ -731,7 +731,9 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
     // literal: lane path when short and staged
     const uint32_t rs = lsrc - (uint32_t)D.s0;
     const uint64_t nlm = wave_ballot(nl != 0u);
-    const uint64_t litm = nlm & wave_ballot(nl <= 16u) & wave_ballot(rs < (uint32_t)kStage) &
+    // (literal runs up to 64 bytes: a lane each, as a match; 16 had been the limit -- runs of
+    // 17..64 then took a whole-wave copy each: -3.1 % decode time with 64, -2.6 % with 32)
+    const uint64_t litm = nlm & wave_ballot(nl <= 64u) & wave_ballot(rs < (uint32_t)kStage) &
                           wave_ballot(rs + nl <= (uint32_t)kStage);
     // match: lane path (window / dst history / dictionary sources, or a self-overlap with
     // offset >= 16 inside the window; a match cut by a segment edge can be shorter than 4)
@@ -761,11 +763,23 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
         coop_literal(L, D, base, lane_val(la, f), lane_val(nl, f), lane_val(lsrc, f));
     }
     wave_sync();
-    if (lane_in(litm)) {
+    if (lane_in(litm)) {   // up to four 16-byte units, the last one ending exactly at nl
         uint8_t *w = L.win + (la - base);
-        const uint4 v = lds16(L.stage + rs);
-        if (nl == 16u) lds_st16(w, v);
-        else lds_put_small<false>(w, v, nl);
+        const uint8_t *sp = L.stage + rs;
+        const uint4 v = lds16(sp);
+        if (nl >= 16u) {
+            const uint32_t t1 = umin(16u, nl - 16u), t2 = umin(32u, nl - 16u), t3 = nl - 16u;
+            uint4 v1, v2, v3;
+            if (nl > 16u) v1 = lds16(sp + t1);
+            if (nl > 32u) v2 = lds16(sp + t2);
+            if (nl > 48u) v3 = lds16(sp + t3);
+            lds_st16(w, v);
+            if (nl > 16u) lds_st16(w + t1, v1);
+            if (nl > 32u) lds_st16(w + t2, v2);
+            if (nl > 48u) lds_st16(w + t3, v3);
+        } else {
+            lds_put_small<false>(w, v, nl);
+        }
     }
     // round 1
     lane_match_store(L, base, lane_in(r1m), ma, nm, off, r1u);
