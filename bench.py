@@ -220,7 +220,8 @@ def e2e_bench(args):
     Compress (TX): pinned host blocks --H2D--> encode --> framed stream
     [le32 c][block]... (frame_offsets + frame_pack) --D2H--> pinned host stream.
     Decompress (RX): pinned framed stream --H2D--> decode straight out of the frames
-    --D2H--> pinned host blocks.  Chunks of `--e2e-chunk` blocks rotate over three
+    --D2H--> pinned host blocks.  Chunks of `--e2e-chunk` blocks (8192 = 512 MiB: a sweep of
+    16384 / 8192 / 4096 measured TX 41.7 / 44.9 / 44.2 GiB/s) rotate over `--e2e-streams`
     streams, each with its own device buffers (stream order protects their reuse), so
     copies in both directions overlap the kernels.  Rates are
     uncompressed bytes / wall time.  Never the headline `value`.
@@ -242,7 +243,7 @@ def e2e_bench(args):
     h_out = torch.empty((nb, n), dtype=torch.uint8, pin_memory=True)
     log("[e2e] pinned %.1f GiB host in %.1f s" % ((2 * nb * n + nb * (slot + 4)) / GIB,
                                                   time.time() - t0))
-    NS = 3
+    NS = args.e2e_streams
     streams = [torch.cuda.Stream() for _ in range(NS)]
     bufs = []
     for _ in range(NS):
@@ -1021,7 +1022,8 @@ def main():
     ap.add_argument("--e2e", action="store_true",
                     help="host->GPU->host socket-path rate instead of the device-resident line")
     ap.add_argument("--e2e-blocks", type=int, default=1 << 17)
-    ap.add_argument("--e2e-chunk", type=int, default=1 << 14)
+    ap.add_argument("--e2e-chunk", type=int, default=1 << 13)
+    ap.add_argument("--e2e-streams", type=int, default=3)
     ap.add_argument("--rand4k", action="store_true",
                     help="BASELINE config 2 alone: decompress-only over 4 KiB random blocks")
     ap.add_argument("--rand4k-blocks", type=int, default=1 << 18)
