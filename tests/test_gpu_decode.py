@@ -437,3 +437,64 @@ def test_final_token_literal_run_ignores_bytes_past_src(cuda, product, oracle):
         exp = [orc_decompress(oracle, b, cap, 10 if partial else None)[0] for b, _, cap in cases]
         assert got == exp, [(c[0], c[2], g, e) for c, g, e in zip(cases, got, exp) if g != e]
         assert all(g == -3 for (b, _, _), g in zip(cases, got) if len(b) == 1), got
+
+
+def test_long_literal_runs_all_modes(cuda, product, oracle):
+    """Round 5 parses a literal length with one extension byte (15..269) in the vector windows:
+    blocks dominated by such runs (and some of 270+, two extension bytes: the scalar path), long
+    enough to restage many times, so runs straddle every staging boundary (a run whose offset
+    bytes lie past the staged input is complex).  decompress_safe at cap n / n - 1 / n + 7, cut
+    short and mutated; _safe_partial at random targets; decompress_fast at n and n - 3; and the
+    same blocks through usingDict with a history dictionary: results and bytes vs the oracle."""
+    import ctypes as C
+    from lz4util import buf
+    from test_gpu_stream import gpu_dict_decode, orc_dict_decode
+    rng = random.Random(2025)
+    blocks = [_dense_block(rng, rng.choice((5, 60, 300, 900)), 0.55, 0.01, 0.2) for _ in range(48)]
+    comps, caps, tg, plains = [], [], [], []
+    for k, (c, out) in enumerate(blocks):
+        for v in range(3):
+            cc = bytearray(c)
+            if v == 1:
+                cc = cc[:rng.randrange(1, len(cc) + 1)]
+            elif v == 2:
+                for _ in range(rng.randrange(1, 3)):
+                    cc[rng.randrange(len(cc))] = rng.randrange(256)
+            comps.append(bytes(cc))
+            caps.append(rng.choice((len(out), len(out) - 1, len(out) + 7)) if v else len(out))
+            tg.append(rng.randrange(0, len(out) + 8))
+            plains.append(out)
+    for targets in (None, tg):
+        rs, outs = run_decode(cuda, product, comps, caps, targets=targets)
+        bad = []
+        for i, (c, cap, r, o) in enumerate(zip(comps, caps, rs, outs)):
+            er, eo = orc_decompress(oracle, c, cap, None if targets is None else targets[i])
+            if r != er or (r > 0 and o != eo[:er] and not _has_off0(c)):
+                bad.append((i, len(c), cap, r, er))
+        assert not bad, bad[:10]
+        if targets is None:   # the unmodified blocks decode in full
+            assert all(rs[3 * k] == len(out) and outs[3 * k] == out for k, (_, out) in enumerate(blocks))
+    # decompress_fast on the valid blocks, exact size and 3 short
+    cases = [(c, len(out) - d) for c, out in blocks for d in (0, 3) if len(out) - d > 0]
+    blobs = [c for c, _ in cases]
+    ins, iptr, _ = pack(cuda, blobs)
+    osz = [n for _, n in cases]
+    dst, dptr, doffs = alloc_out(cuda, osz)
+    res = ints(cuda, [0] * len(cases))
+    product.decompress_fast_ptr_batch(iptr, ints(cuda, [len(b) for b in blobs]), dptr,
+                                      ints(cuda, osz), res)
+    cuda.cuda.synchronize()
+    rs = res.cpu().tolist()
+    for i, (c, n) in enumerate(cases):
+        o = C.create_string_buffer(max(n, 1) + 64)
+        er = oracle.orc_decompress_fast(buf(c), o, n)
+        assert rs[i] == er, (i, n, len(c), rs[i], er)
+        if er > 0:
+            assert fetch(dst, doffs[i], n) == o.raw[:n], i
+    # usingDict: the same blocks after a random history (matches stay inside their own output)
+    dicts = [bytes(rng.randrange(256) for _ in range(rng.choice((0, 100, 5000, 70000))))
+             for _ in blocks]
+    got = gpu_dict_decode(cuda, product, [c for c, _ in blocks], [len(o) for _, o in blocks],
+                          dicts, False)
+    for (c, out), d, g in zip(blocks, dicts, got):
+        assert g == orc_dict_decode(oracle, c, len(out), d) == (len(out), out)
