@@ -113,20 +113,8 @@ __device__ __forceinline__ uint32_t shash(uint32_t x, uint32_t b4) {
 }
 
 // 16 / 4 bytes at byte address x of the block buffer.  Default: single unaligned LDS reads
-// (gfx950 serves any alignment); APE_SEG_ALIGNED_READS: aligned dword reads + v_alignbyte.
-#ifdef APE_SEG_ALIGNED_READS
-__device__ __forceinline__ uint4 lds16(const SegLds &S, uint32_t x) {
-    const uint32_t *r = S.blk + (x >> 2);
-    const uint32_t sh = x & 3u;
-    const uint32_t w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3], w4 = r[4];
-    return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                      __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
-}
-__device__ __forceinline__ uint32_t lds4(const SegLds &S, uint32_t x) {
-    const uint32_t *r = S.blk + (x >> 2);
-    return __builtin_amdgcn_alignbyte(r[1], r[0], x & 3u);
-}
-#else
+// (gfx950 serves any alignment; aligned dword reads + v_alignbyte were measured no faster,
+// and an 8-byte prefilter choosing one of the four candidates -3.5 % time for ratio 3.39 -> 3.19).
 typedef uint32_t l32x4 __attribute__((ext_vector_type(4), aligned(1)));
 typedef uint32_t l32x4a2 __attribute__((ext_vector_type(4), aligned(2)));
 typedef uint32_t l32 __attribute__((aligned(1)));
@@ -138,7 +126,6 @@ __device__ __forceinline__ uint4 lds16(const SegLds &S, uint32_t x) {
 __device__ __forceinline__ uint32_t lds4(const SegLds &S, uint32_t x) {
     return *(const l32 *)((const uint8_t *)S.blk + x);
 }
-#endif
 __device__ __forceinline__ uint32_t ldsb(const SegLds &S, uint32_t x) {
     return ((const uint8_t *)S.blk)[x];
 }
@@ -468,24 +455,6 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
                 }
                 const int room = capE - q;
                 int best = 0, bestc = 0;
-#ifdef APE_SEG_PICK8   // measured: -3.5 % kernel time for ratio 3.39 -> 3.19 (not kept)
-                // the four latest candidates, prefiltered on 8 bytes: the first (latest) that
-                // matches 8 bytes, else the first that matches 4, is measured over 16 bytes
-                int cpick = 0, lvl = 0;   // lvl: 2 = 8 bytes equal, 1 = 4 bytes
-#pragma unroll
-                for (int d = kSDepth - 1; d >= 0; d--) {   // latest last: it wins ties
-                    const int j = lb - 1 - d;
-                    const int c = (int)((r4 >> (48 - 16 * d)) & 0xFFFFu);
-                    const l32x2 v = *(const l32x2 *)((const uint8_t *)S.blk + a0 + (uint32_t)c);
-                    const int lv = (j >= wlo && c < q && v.x == own.x) ? (v.y == own.y ? 2 : 1) : 0;
-                    if (lv > 0 && lv >= lvl) { lvl = lv; cpick = c; }
-                }
-                if (lvl && room >= kMinMatch) {
-                    int l = (int)prefix16(own, lds16(S, a0 + (uint32_t)cpick));
-                    best = l < room ? l : room;
-                    bestc = cpick;
-                }
-#else
                 // the four latest candidates; those whose first 4 bytes match are measured,
                 // one at a time per lane (a loop as long as the lane with the most of them)
                 int cd[kSDepth];
@@ -505,7 +474,6 @@ __global__ void __launch_bounds__(kSThreads) lz4_encode_seg_kernel(BlockArgs a) 
                     l = l < room ? l : room;
                     if (l > best) { best = l; bestc = c; }
                 }
-#endif
                 if (best < kMinMatch) {
                     q++;
                 } else {
