@@ -700,6 +700,20 @@ __device__ __forceinline__ void lane_match_store(WaveLds &L, uint32_t base, bool
     }
 }
 
+// Copy sub-phase timers (diagnostic stats build only): cycles of the slides, the segment's
+// ballots + literals, round 1, the dependent passes and the flushes.
+#ifdef APE_LZ4_STATS
+#define SUB_P , uint64_t *sub_
+#define SUB_A , sub_
+#define SUB_START uint64_t sub_t_ = clock64();
+#define SUB_MARK(i) do { const uint64_t t_ = clock64(); sub_[i] += t_ - sub_t_; sub_t_ = t_; } while (0)
+#else
+#define SUB_P
+#define SUB_A
+#define SUB_START
+#define SUB_MARK(i) do {} while (0)
+#endif
+
 // Per-lane sequence of the batch: literal [o, m) from input ls, match [m, me) at offset off.
 struct Seq {
     uint32_t o, m, me, ls, off;
@@ -713,7 +727,8 @@ struct Seq {
 // pending sequence is a whole-wave item (everything before it is done): it runs then.
 template <bool DICT>
 __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win &W, const Seq &q,
-                                             uint32_t S0, uint32_t S1, uint32_t &diag) {
+                                             uint32_t S0, uint32_t S1, uint32_t &diag SUB_P) {
+    SUB_START
     const int lane = D.lane;
     const uint32_t base = W.base;
     const uint32_t la = umax(q.o, S0), lb = umin(q.m, S1);
@@ -782,8 +797,10 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
         }
     }
     // round 1
+    SUB_MARK(1);
     lane_match_store(L, base, lane_in(r1m), ma, nm, off, r1u);
     uint64_t pm = mpm & ~r1m;
+    SUB_MARK(2);
     if (!pm) return;
     // sequences owning [max(ps, S0), pe): k0 = owner(first byte), k1 = owner(last byte),
     // by binary search over the sequence starts (lanes past the batch hold B1)
@@ -816,6 +833,7 @@ __device__ __forceinline__ void copy_segment(WaveLds &L, const Dec &D, const Win
         if (!(pm & ~done)) break;
         wave_sync();
     }
+    SUB_MARK(3);
 }
 
 // Write window bytes [fl, F1) to dst: F1 = S1 rounded down to a 16-byte dst address
@@ -871,7 +889,7 @@ __device__ __forceinline__ void slide(WaveLds &L, const Dec &D, Win &W, uint32_t
 // Copy the batch's output [B0, B1) (nd descriptors) through the window to dst.
 template <bool DICT>
 __device__ __forceinline__ void copy_batch(WaveLds &L, const Dec &D, Win &W, int nd, uint32_t B0,
-                                           uint32_t B1, bool last, uint32_t &diag) {
+                                           uint32_t B1, bool last, uint32_t &diag SUB_P) {
     const int lane = D.lane;
     wave_sync();
     const bool has = lane < nd;
@@ -885,12 +903,18 @@ __device__ __forceinline__ void copy_batch(WaveLds &L, const Dec &D, Win &W, int
     q.off = d.w;
     for (uint32_t S0 = B0; S0 < B1;) {
         if (B1 > W.base + kWinB && S0 >= W.base + kKeep + 16u) {
+            SUB_START
             slide(L, D, W, (S0 - kKeep) & ~15u, S0);
+            SUB_MARK(0);
             diag += 1u << 24;
         }
         const uint32_t S1 = umin(B1, W.base + kWinB);
-        copy_segment<DICT>(L, D, W, q, S0, S1, diag);
-        flush(L, D, W, S1, last && S1 == B1);
+        copy_segment<DICT>(L, D, W, q, S0, S1, diag SUB_A);
+        {
+            SUB_START
+            flush(L, D, W, S1, last && S1 == B1);
+            SUB_MARK(4);
+        }
         S0 = S1;
     }
     if (last) flush(L, D, W, B1, true);
@@ -1003,6 +1027,9 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
     }
 
     STATS_DECL
+#ifdef APE_LZ4_STATS
+    uint64_t sub_[5] = {0, 0, 0, 0, 0};
+#endif
     int P = 0;               // next token (wave-uniform)
     uint32_t op = 0;         // its output position
     int result = 0;
@@ -1055,7 +1082,7 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
             const uint32_t B1 = nc < nd ? (uint32_t)__builtin_amdgcn_readfirstlane(L.desc[nc].y) : op;
             const bool last = st == ST_DONE && nc == nd;
             uint32_t diag = 0;
-            copy_batch<DICT>(L, D, W, nc, cst, B1, last, diag);
+            copy_batch<DICT>(L, D, W, nc, cst, B1, last, diag SUB_A);
             STAT_ADD(3, diag & 0xFFFFu);          // wave passes after round 1
             STAT_ADD(5, (diag >> 16) & 0xFFu);    // coop matches
             STAT_ADD(6, diag >> 24);              // window slides
@@ -1081,6 +1108,13 @@ __device__ __forceinline__ void decode_block(WaveLds &L, const BlockArgs &a, con
     }
     if (lane == 0) a.result[b] = result;
     STAT_ADD(10, 1);
+#ifdef APE_LZ4_STATS
+    STAT_ADD(7, sub_[0]);    // slides
+    STAT_ADD(8, sub_[1]);    // segment ballots + literals
+    STAT_ADD(9, sub_[2]);    // round 1
+    STAT_ADD(11, sub_[3]);   // dependent passes
+    STAT_ADD(12, sub_[4]);   // flushes
+#endif
     STATS_FLUSH(g_dec_stats);
 }
 

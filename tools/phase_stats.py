@@ -14,8 +14,8 @@ os.environ.setdefault("APE_LZ4_LIB", os.path.join(ROOT, "libapenetwork_amd", "li
 sys.path.insert(0, ROOT)
 
 DEC = ["parse", "copy", "(batches)", "(passes after round 1)", "(restages)", "(coop matches)",
-       "(window slides)", "", "", "", "(blocks)", "(pending matches)", "(in one owner's match)",
-       "(... its bytes from before S0)", "", ""]
+       "(window slides)", "[copy] slides", "[copy] ballots + literals", "[copy] round 1", "(blocks)",
+       "[copy] dependent passes", "[copy] flushes", "", "", ""]
 ENC = ["W walk", "W publish", "E write", "W wait end", "W wait mid", "P A+B+C1",
        "P wait mid", "P C2 + S2 + R", "P wait end", "P load waits", "(steps x3 waves)",
        "(members)", "E prepare",
@@ -56,7 +56,8 @@ def main():
         blocks = vals[labels.index("(blocks)")]
         print("%s: %d blocks, %.2f ms, %.1f GB/s (in+out bytes)" % (
             name, nb, ms, (nb * n + int(csz.sum())) / ms / 1e6))
-        tot = sum(v for i, v in enumerate(vals) if labels[i] and not labels[i].startswith("(") and labels[i] != "-")
+        tot = sum(v for i, v in enumerate(vals)
+                  if labels[i] and not labels[i].startswith(("(", "[")) and labels[i] != "-")
         for i, lab in enumerate(labels):
             if not lab or lab == "-":
                 continue
