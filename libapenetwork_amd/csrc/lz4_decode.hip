@@ -16,7 +16,8 @@
 //         member its output position, and every member applies the reference's
 //         checks (:1345-1444) in the reference's order, so the first failing
 //         sequence returns the identical -(ip)-1.  Rare "complex" tokens
-//         (literal length >= 15, or a match length needing > 1 extension byte)
+//         (a literal or match length needing more than one extension byte, or a
+//         long literal run whose offset lies past the staged input)
 //         are parsed by the scalar restatement of the reference loop instead.
 //         Accepted sequences become descriptors {literal source, output
 //         position, literal length, offset} in LDS.
