@@ -22,11 +22,12 @@
 //         Accepted sequences become descriptors {literal source, output
 //         position, literal length, offset} in LDS.
 //  COPY   One lane per sequence: the batch's output is assembled in an LDS window
-//         of recent output.  Round 1: every lane writes its literal run (16-byte
-//         LDS read from the staged input, exact-length write) and its match when the
-//         match's sources precede the batch -- up to four 16-byte units read from the
-//         window, or from dst history (flushed, drained, read bypassing this CU's L1),
-//         or the external dictionary.  Matches whose sources lie inside the batch wait
+//         of recent output.  Round 1: every lane writes its literal run (up to 64
+//         bytes: four 16-byte units from the staged input, the last one ending
+//         exactly) and its match when the match's sources precede the batch -- up to
+//         four 16-byte units read from the window, or from dst history (flushed,
+//         drained, read bypassing this CU's L1; issued before the literals are
+//         written), or the external dictionary.  Matches whose sources lie inside the batch wait
 //         for the rounds that follow: everything before the first pending sequence is
 //         final, so each round copies every pending match whose sources end there.
 //         Long runs, offsets < 16 inside their own output and sources straddling the
