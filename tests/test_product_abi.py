@@ -198,6 +198,11 @@ def test_no_gpu_fails_loudly(product):
     # the batch API has no host path at all
     z = C.c_void_p(0)
     assert L.APE_LZ4_compress_batch_dev(z, z, z, z, z, 1, z) != 0
+    # argument checks come before the device check (EINVAL = -2), then ENODEV (-1)
+    assert L.APE_LZ4_compress_exact_batch_dev(z, z, z, z, z, -1, 1, z) == -2
+    assert L.APE_LZ4_compress_exact_batch_dev(z, z, z, z, z, 3, 1, z) == -2
+    p = C.c_void_p(8)   # never dereferenced: no device
+    assert L.APE_LZ4_compress_exact_batch_dev(p, p, p, p, p, 3, 1, z) == -1
 
 
 def test_one_shot_compress_above_gpu_block(product, golden, oracle):
