@@ -3,7 +3,7 @@
 blocks for the library APE_LZ4_LIB names (a variant built by tools/src_variant.sh or make variant);
 for variants whose output is not a valid block (sensitivity builds), where tools/ab_inproc.py stops."""
 import os, sys, torch
-sys.path.insert(0, os.environ["GRAFT_REPO_ROOT"])
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import libapenetwork_amd as amd
 nb, n = 131072, 65536
 slot = (amd.compressBound(n) + 15) // 16 * 16
