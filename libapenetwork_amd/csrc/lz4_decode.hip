@@ -319,6 +319,29 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
     return z;
 }
 
+// The hop alone of the sequence at window position rel (chain_at): as spec_at, but the offset
+// is not needed -- only the match-length extension byte, one byte read (every lane reads it,
+// only a nibble-15 lane uses it; no further than spec_at's 8-byte read, and a position past the
+// staged input only ever belongs to a complex lane, whose bytes do not matter).  Against the full spec_at here: -0.5 % decode time
+// (profiles/r5_decoder_hop_ab.txt).
+constexpr uint32_t kHopTerm = 0x200u, kHopCplx = 0x300u;   // chain_at's exit codes (below)
+template <bool FASTD>
+__device__ __forceinline__ uint32_t hop_at(const WaveLds &L, const Dec &D, int P, uint32_t rel) {
+    const uint32_t r = (uint32_t)(P - D.s0) + rel;
+    const uint32_t tok = L.stage[r], e1 = L.stage[r + 1u];
+    const bool litx = tok >= 0xF0u;
+    const uint32_t lit = litx ? 15u + e1 : tok >> 4;
+    const bool mlx = (tok & 15u) == 15u;
+    const uint32_t r1 = r + 1u + (litx ? 1u : 0u) + lit;
+    const int lim = D.csize - D.s0;
+    const bool fin_in = !FASTD && (int)r1 > lim - 8;
+    const bool mlerr = !FASTD && mlx && (int)r1 > lim - 2 - kLastLiterals;
+    const uint32_t e = L.stage[r1 + 2u];
+    const bool cx = (litx && (e1 == 255u || r1 + 3u > (uint32_t)kStage)) || (mlx && e == 255u && !mlerr);
+    const uint32_t qr = r1 - (uint32_t)(P - D.s0) + (mlx ? 3u : 2u);
+    return cx ? kHopCplx : (fin_in ? kHopTerm : qr);
+}
+
 // The chain of sequences from window position 0 of a window at P: every lane parses
 // "the sequence at P + lane" and its successor (hop).  The true chain is found by binary
 // lifting instead of a serial walk: J_k = hop^(2^k) (four ds_bpermute rounds), and lane t
@@ -327,7 +350,6 @@ __device__ __forceinline__ Spec spec_at(const WaveLds &L, const Dec &D, int P, u
 // (lanes [0, cnt)); X = the chain's exit (next token position >= 64, or kHopTerm after a
 // final / failing sequence, kHopCplx before a complex token); lastp = the last member.
 // A real hop is < 0x200 (63 + 1 + 1 + 269 + 2 + 1); the codes are above it.
-constexpr uint32_t kHopTerm = 0x200u, kHopCplx = 0x300u;
 template <bool FASTD>
 __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, uint32_t &pos,
                                          int &cnt, uint32_t &X, uint32_t &lastp) {
@@ -337,9 +359,7 @@ __device__ __forceinline__ void chain_at(const WaveLds &L, const Dec &D, int P, 
     {
         // the hop alone: mlerr implies fin_in (ipo + 5 = ipl + lit + 7), and the successor
         // relative to P is the staged position after the literals + 2 (+1 with the ml byte)
-        const Spec z = spec_at<FASTD>(L, D, P, (uint32_t)D.lane);
-        const uint32_t qr = z.r1 - (uint32_t)(P - D.s0) + (z.mlx ? 3u : 2u);
-        hop = 4u * (z.cx ? kHopCplx : (z.fin_in ? kHopTerm : qr));
+        hop = 4u * hop_at<FASTD>(L, D, P, (uint32_t)D.lane);
     }
     // Exits absorb as a max: a real hop moves forward (J[a] > a), and an exit (>= 256) reads
     // some lane's J through the address wrap but max keeps it >= 256.  A jump from a real
