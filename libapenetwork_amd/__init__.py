@@ -190,13 +190,92 @@ def _check(rc, what):
         raise GpuError("%s failed (%d): %s" % (what, rc, gpu_last_error()))
 
 
+# ---- argument checks: every pointer handed to C comes from a tensor of the dtype, device and
+# layout the C signature assumes; ValueError before any call ----
+def _arr(t, what, dtype, n=None, optional=False, cuda=True):
+    """A contiguous 1-D CUDA tensor of `dtype` (and length n when given)."""
+    import torch
+    if t is None and optional:
+        return
+    if not isinstance(t, torch.Tensor):
+        raise ValueError("%s: need a torch tensor" % what)
+    if t.dtype != dtype:
+        raise ValueError("%s: dtype %s, need %s" % (what, t.dtype, dtype))
+    if t.dim() != 1 or not t.is_contiguous():
+        raise ValueError("%s: need a contiguous 1-D tensor" % what)
+    if n is not None and t.shape[0] != n:
+        raise ValueError("%s: %d elements, need %d" % (what, t.shape[0], n))
+    if cuda:
+        _on_cuda(what, t)
+
+
+def _rows(t, what, n=None, cuda=True):
+    """A 2-D uint8 CUDA tensor whose rows are contiguous (row i at data_ptr + i * stride(0),
+    shape[1] bytes each, rows not overlapping)."""
+    import torch
+    if not isinstance(t, torch.Tensor):
+        raise ValueError("%s: need a torch tensor" % what)
+    if t.dtype != torch.uint8:
+        raise ValueError("%s: dtype %s, need torch.uint8" % (what, t.dtype))
+    if t.dim() != 2:
+        raise ValueError("%s: need a 2-D tensor [blocks, bytes]" % what)
+    if (t.shape[1] > 1 and t.stride(1) != 1) or (t.shape[0] > 1 and t.stride(0) < t.shape[1]):
+        raise ValueError("%s: rows must be contiguous and not overlap" % what)
+    if n is not None and t.shape[0] != n:
+        raise ValueError("%s: %d rows, need %d" % (what, t.shape[0], n))
+    if cuda:
+        _on_cuda(what, t)
+
+
+def _on_cuda(what, *ts):
+    for t in ts:
+        if t is not None and t.device.type != "cuda":
+            raise ValueError("%s: need CUDA tensors" % what)
+
+
+def _strided_args(src, sizes, dst, results, caps, what):
+    """compress_batch / decompress_batch: the C side reads block i at src + i*stride(0) and
+    writes dst + i*stride(0) with capacity caps[i] or, without caps, stride(0) -- so a row
+    narrower than its stride needs explicit caps."""
+    import torch
+    _rows(src, what + " src", cuda=False)
+    n = src.shape[0]
+    _rows(dst, what + " dst", n, cuda=False)
+    _arr(sizes, what + " sizes", torch.int32, n, cuda=False)
+    _arr(results, what + " results", torch.int32, n, cuda=False)
+    _arr(caps, what + " dst_caps", torch.int32, n, optional=True, cuda=False)
+    if caps is None and n > 0 and dst.shape[1] != dst.stride(0):
+        raise ValueError("%s: dst rows narrower than their stride need dst_caps" % what)
+    _on_cuda(what, src, dst, sizes, results, caps)
+    return n
+
+
+def _ptr_args(what, n, **arrs):
+    """Pointer-array calls: name -> (tensor, dtype) of N elements each (int64 pointers, int32
+    sizes); a None tensor is allowed where dtype is given as (dtype, True)."""
+    for name, (t, spec) in arrs.items():
+        dtype, opt = spec if isinstance(spec, tuple) else (spec, False)
+        _arr(t, "%s %s" % (what, name), dtype, n, optional=opt, cuda=False)
+    _on_cuda(what, *(t for t, _ in arrs.values()))
+
+
+def _i64():
+    import torch
+    return torch.int64
+
+
+def _i32():
+    import torch
+    return torch.int32
+
+
 def compress_batch(src, src_sizes, dst, results, dst_caps=None, stream=None):
     """N x APE_LZ4_compress_default on device.
 
     src: uint8 [N, S] CUDA tensor (block i = row i, first src_sizes[i] bytes);
     dst: uint8 [N, D] CUDA tensor; results: int32 [N] (compressed size or 0).
     """
-    n = src.shape[0]
+    n = _strided_args(src, src_sizes, dst, results, dst_caps, "compress_batch")
     _check(lib().APE_LZ4_compress_batch_strided_dev(
         _ptr(src), src.stride(0), _ptr(src_sizes), _ptr(dst), dst.stride(0), _ptr(dst_caps),
         _ptr(results), n, _stream(stream)), "APE_LZ4_compress_batch_strided_dev")
@@ -204,7 +283,7 @@ def compress_batch(src, src_sizes, dst, results, dst_caps=None, stream=None):
 
 def decompress_batch(comp, comp_sizes, dst, results, dst_caps=None, stream=None):
     """N x APE_LZ4_decompress_safe on device (caps default to dst row stride)."""
-    n = comp.shape[0]
+    n = _strided_args(comp, comp_sizes, dst, results, dst_caps, "decompress_batch")
     _check(lib().APE_LZ4_decompress_safe_batch_strided_dev(
         _ptr(comp), comp.stride(0), _ptr(comp_sizes), _ptr(dst), dst.stride(0), _ptr(dst_caps),
         _ptr(results), n, _stream(stream)), "APE_LZ4_decompress_safe_batch_strided_dev")
@@ -214,6 +293,9 @@ def decompress_partial_batch(src_ptrs, comp_sizes, dst_ptrs, targets, caps, resu
                              stream=None):
     """N x APE_LZ4_decompress_safe_partial, pointer-array form (int64 tensors of pointers)."""
     n = comp_sizes.shape[0]
+    _ptr_args("decompress_partial_batch", n, src_ptrs=(src_ptrs, _i64()), comp_sizes=(comp_sizes, _i32()),
+              dst_ptrs=(dst_ptrs, _i64()), targets=(targets, _i32()), caps=(caps, _i32()),
+              results=(results, _i32()))
     _check(lib().APE_LZ4_decompress_safe_partial_batch_dev(
         _ptr(src_ptrs), _ptr(comp_sizes), _ptr(dst_ptrs), _ptr(targets), _ptr(caps),
         _ptr(results), n, _stream(stream)), "APE_LZ4_decompress_safe_partial_batch_dev")
@@ -223,6 +305,8 @@ def compress_fast_ptr_batch(src_ptrs, src_sizes, dst_ptrs, caps, results, accele
                             stream=None):
     """N x APE_LZ4_compress_fast, pointer-array form (int64 tensors of pointers)."""
     n = src_sizes.shape[0]
+    _ptr_args("compress_fast_ptr_batch", n, src_ptrs=(src_ptrs, _i64()), src_sizes=(src_sizes, _i32()),
+              dst_ptrs=(dst_ptrs, _i64()), caps=(caps, _i32()), results=(results, _i32()))
     _check(lib().APE_LZ4_compress_fast_batch_dev(
         _ptr(src_ptrs), _ptr(src_sizes), _ptr(dst_ptrs), _ptr(caps), _ptr(results), n,
         acceleration, _stream(stream)), "APE_LZ4_compress_fast_batch_dev")
@@ -233,6 +317,8 @@ def compress_exact_ptr_batch(src_ptrs, src_sizes, dst_ptrs, caps, results, accel
     """Greedy-exact mode: N x APE_LZ4_compress_fast byte for byte (the reference's own
     sequential parse, one wave per block; slow, for debugging)."""
     n = src_sizes.shape[0]
+    _ptr_args("compress_exact_ptr_batch", n, src_ptrs=(src_ptrs, _i64()), src_sizes=(src_sizes, _i32()),
+              dst_ptrs=(dst_ptrs, _i64()), caps=(caps, _i32()), results=(results, _i32()))
     _check(lib().APE_LZ4_compress_exact_batch_dev(
         _ptr(src_ptrs), _ptr(src_sizes), _ptr(dst_ptrs), _ptr(caps), _ptr(results), n,
         acceleration, _stream(stream)), "APE_LZ4_compress_exact_batch_dev")
@@ -242,6 +328,9 @@ def compress_destSize_ptr_batch(src_ptrs, src_sizes, dst_ptrs, targets, results,
     """N x APE_LZ4_compress_destSize, pointer-array form: src_sizes (int32) is in/out --
     input sizes on entry, consumed input bytes on return; results = bytes written."""
     n = src_sizes.shape[0]
+    _ptr_args("compress_destSize_ptr_batch", n, src_ptrs=(src_ptrs, _i64()),
+              src_sizes=(src_sizes, _i32()), dst_ptrs=(dst_ptrs, _i64()), targets=(targets, _i32()),
+              results=(results, _i32()))
     _check(lib().APE_LZ4_compress_destSize_batch_dev(
         _ptr(src_ptrs), _ptr(src_sizes), _ptr(dst_ptrs), _ptr(targets), _ptr(results), n,
         _stream(stream)), "APE_LZ4_compress_destSize_batch_dev")
@@ -252,6 +341,11 @@ def compress_destSize_scratch_ptr_batch(src_ptrs, src_sizes, dst_ptrs, targets, 
     """compress_destSize_ptr_batch with caller-owned scratch (uint8 CUDA tensor of at least
     destSize_scratch_size(1) bytes): allocates nothing, so it can be graph-captured."""
     n = src_sizes.shape[0]
+    _ptr_args("compress_destSize_scratch_ptr_batch", n, src_ptrs=(src_ptrs, _i64()),
+              src_sizes=(src_sizes, _i32()), dst_ptrs=(dst_ptrs, _i64()), targets=(targets, _i32()),
+              results=(results, _i32()))
+    import torch
+    _arr(scratch, "compress_destSize_scratch_ptr_batch scratch", torch.uint8)
     _check(lib().APE_LZ4_compress_destSize_batch_scratch_dev(
         _ptr(src_ptrs), _ptr(src_sizes), _ptr(dst_ptrs), _ptr(targets), _ptr(results), n,
         _ptr(scratch), scratch.numel(), _stream(stream)),
@@ -266,6 +360,9 @@ def decompress_fast_ptr_batch(src_ptrs, src_bounds, dst_ptrs, original_sizes, re
                               stream=None):
     """N x APE_LZ4_decompress_fast, pointer-array form: results = input bytes consumed."""
     n = original_sizes.shape[0]
+    _ptr_args("decompress_fast_ptr_batch", n, src_ptrs=(src_ptrs, _i64()),
+              src_bounds=(src_bounds, _i32()), dst_ptrs=(dst_ptrs, _i64()),
+              original_sizes=(original_sizes, _i32()), results=(results, _i32()))
     _check(lib().APE_LZ4_decompress_fast_batch_dev(
         _ptr(src_ptrs), _ptr(src_bounds), _ptr(dst_ptrs), _ptr(original_sizes), _ptr(results),
         n, _stream(stream)), "APE_LZ4_decompress_fast_batch_dev")
@@ -274,6 +371,8 @@ def decompress_fast_ptr_batch(src_ptrs, src_bounds, dst_ptrs, original_sizes, re
 def decompress_ptr_batch(src_ptrs, comp_sizes, dst_ptrs, caps, results, stream=None):
     """N x APE_LZ4_decompress_safe, pointer-array form."""
     n = comp_sizes.shape[0]
+    _ptr_args("decompress_ptr_batch", n, src_ptrs=(src_ptrs, _i64()), comp_sizes=(comp_sizes, _i32()),
+              dst_ptrs=(dst_ptrs, _i64()), caps=(caps, _i32()), results=(results, _i32()))
     _check(lib().APE_LZ4_decompress_safe_batch_dev(
         _ptr(src_ptrs), _ptr(comp_sizes), _ptr(dst_ptrs), _ptr(caps), _ptr(results), n,
         _stream(stream)), "APE_LZ4_decompress_safe_batch_dev")
@@ -284,6 +383,9 @@ def compress_prefix_batch(src_ptrs, src_sizes, prefix_sizes, dst_ptrs, caps, res
     """N chained-stream chunks (compress_fast_continue on a stream whose history is the
     prefix_sizes[i] bytes just before src_ptrs[i]); pointer-array form (int64 tensors)."""
     n = src_sizes.shape[0]
+    _ptr_args("compress_prefix_batch", n, src_ptrs=(src_ptrs, _i64()), src_sizes=(src_sizes, _i32()),
+              prefix_sizes=(prefix_sizes, _i32()), dst_ptrs=(dst_ptrs, _i64()),
+              caps=(caps, _i32()), results=(results, _i32()))
     _check(lib().APE_LZ4_compress_withPrefix_batch_dev(
         _ptr(src_ptrs), _ptr(src_sizes), _ptr(prefix_sizes), _ptr(dst_ptrs), _ptr(caps),
         _ptr(results), n, _stream(stream)), "APE_LZ4_compress_withPrefix_batch_dev")
@@ -293,6 +395,9 @@ def decompress_dict_batch(src_ptrs, comp_sizes, dst_ptrs, caps, dict_ptrs, dict_
                           stream=None):
     """N x APE_LZ4_decompress_safe_usingDict, pointer-array form (int64 tensors)."""
     n = comp_sizes.shape[0]
+    _ptr_args("decompress_dict_batch", n, src_ptrs=(src_ptrs, _i64()), comp_sizes=(comp_sizes, _i32()),
+              dst_ptrs=(dst_ptrs, _i64()), caps=(caps, _i32()), dict_ptrs=(dict_ptrs, _i64()),
+              dict_sizes=(dict_sizes, _i32()), results=(results, _i32()))
     _check(lib().APE_LZ4_decompress_safe_usingDict_batch_dev(
         _ptr(src_ptrs), _ptr(comp_sizes), _ptr(dst_ptrs), _ptr(caps), _ptr(dict_ptrs),
         _ptr(dict_sizes), _ptr(results), n, _stream(stream)),
@@ -301,6 +406,10 @@ def decompress_dict_batch(src_ptrs, comp_sizes, dst_ptrs, caps, dict_ptrs, dict_
 
 def synth_blocks(dst, block_size, first_block, kind, stream=None):
     """Fill rows of uint8 [N, S] CUDA tensor with SURVEY App. C blocks (kind 0 rand, 1 comp)."""
+    _rows(dst, "synth_blocks dst", cuda=False)
+    if not 0 <= block_size <= dst.shape[1]:
+        raise ValueError("synth_blocks: block_size must fit a row")
+    _on_cuda("synth_blocks", dst)
     _check(lib().APE_LZ4_synth_blocks_dev(_ptr(dst), dst.stride(0), block_size, first_block,
                                           dst.shape[0], kind, _stream(stream)),
            "APE_LZ4_synth_blocks_dev")
@@ -310,7 +419,14 @@ def synth_blocks(dst, block_size, first_block, kind, stream=None):
 def frame_offsets(comp_sizes, offsets, scratch=None, stream=None):
     """offsets (int64 [N+1] CUDA) <- exclusive scan of 4 + comp_sizes[i]; returns scratch."""
     import torch
+    _arr(comp_sizes, "frame_offsets comp_sizes", torch.int32, cuda=False)
     n = comp_sizes.shape[0]
+    _arr(offsets, "frame_offsets offsets", torch.int64, n + 1, cuda=False)
+    if scratch is not None:
+        _arr(scratch, "frame_offsets scratch", torch.uint8, cuda=False)
+        if scratch.numel() < lib().APE_LZ4_frame_scratch_size(n):
+            raise ValueError("frame_offsets: scratch smaller than APE_LZ4_frame_scratch_size")
+    _on_cuda("frame_offsets", comp_sizes, offsets, scratch)
     if scratch is None:
         nbytes = lib().APE_LZ4_frame_scratch_size(n)
         scratch = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=comp_sizes.device)
@@ -321,7 +437,13 @@ def frame_offsets(comp_sizes, offsets, scratch=None, stream=None):
 
 def frame_pack(comp, comp_sizes, offsets, frames, stream=None):
     """Framed stream [le32 c][c bytes]... of the compressed rows of comp (uint8 [N, D])."""
-    n = comp_sizes.shape[0]
+    import torch
+    _rows(comp, "frame_pack comp", cuda=False)
+    n = comp.shape[0]
+    _arr(comp_sizes, "frame_pack comp_sizes", torch.int32, n, cuda=False)
+    _arr(offsets, "frame_pack offsets", torch.int64, n + 1, cuda=False)
+    _arr(frames, "frame_pack frames", torch.uint8, cuda=False)
+    _on_cuda("frame_pack", comp, comp_sizes, offsets, frames)
     _check(lib().APE_LZ4_frame_pack_strided_dev(_ptr(comp), comp.stride(0), _ptr(comp_sizes),
                                                 _ptr(offsets), _ptr(frames), n, _stream(stream)),
            "APE_LZ4_frame_pack_strided_dev")
@@ -329,7 +451,25 @@ def frame_pack(comp, comp_sizes, offsets, frames, stream=None):
 
 def decompress_frames(frames, offsets, dst, results, dst_caps=None, nblocks=None, stream=None):
     """N x APE_LZ4_decompress_safe of the blocks of a framed stream into rows of dst."""
+    import torch
+    _rows(dst, "decompress_frames dst", cuda=False)
     n = dst.shape[0] if nblocks is None else nblocks
+    if not 0 <= n <= dst.shape[0]:
+        raise ValueError("decompress_frames: nblocks must be within dst's rows")
+    _arr(frames, "decompress_frames frames", torch.uint8, cuda=False)
+    _arr(offsets, "decompress_frames offsets", torch.int64, cuda=False)
+    if offsets.shape[0] < n + 1:
+        raise ValueError("decompress_frames: offsets need nblocks + 1 entries")
+    _arr(results, "decompress_frames results", torch.int32, cuda=False)
+    if results.shape[0] < n:
+        raise ValueError("decompress_frames: results need nblocks entries")
+    if dst_caps is not None:
+        _arr(dst_caps, "decompress_frames dst_caps", torch.int32, cuda=False)
+        if dst_caps.shape[0] < n:
+            raise ValueError("decompress_frames: dst_caps need nblocks entries")
+    elif n > 0 and dst.shape[1] != dst.stride(0):
+        raise ValueError("decompress_frames: dst rows narrower than their stride need dst_caps")
+    _on_cuda("decompress_frames", frames, offsets, dst, results, dst_caps)
     _check(lib().APE_LZ4_decompress_safe_frames_dev(_ptr(frames), _ptr(offsets), _ptr(dst),
                                                     dst.stride(0), _ptr(dst_caps), _ptr(results),
                                                     n, _stream(stream)),

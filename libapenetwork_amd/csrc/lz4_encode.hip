@@ -41,7 +41,6 @@
 //     with one 16-byte store per lane; the last literals (:732-751) are copied with
 //     16-byte moves.
 #include "lz4_gpu_internal.h"
-#include <stdlib.h>
 #include <type_traits>
 
 namespace apelz4 {
@@ -72,6 +71,25 @@ constexpr int kHLog = APE_LZ4_HLOG;
 // <= 72 VGPRs).  Measured on 131072 blocks: 6912 entries -4.6 % encode time vs 8192, ratio
 // 3.1464 -> 3.1279; 7200 (once the info array was single-buffered) 3.1329 at the same time
 // (tools/enc_model.c models the ratio per table size).
+// Hash key: the bytes the table hash covers (the reference: 5, :456-473).  7 by default, with
+// every position in the table (kAllPos): the longer key keeps short chance matches from
+// pre-empting longer ones -- ratio above the round-5 encoder's on App. C data and on real
+// files, 23 % fewer sequences (tools/enc_model.c key study)
+#ifndef APE_LZ4_HKEY
+#define APE_LZ4_HKEY 7
+#endif
+constexpr int kKey = APE_LZ4_HKEY;
+static_assert(kKey >= 5 && kKey <= 8, "hash key of 5..8 bytes");
+// Table inserts: 1 = the producer writes every hashable position of a chunk into the table
+// right after the chunk's lookups (no lag: chunk k sees every position of chunks < k, and the
+// walker inserts nothing); 0 = the reference's policy (:595-619, :680-706), walked positions
+// and match_end - 2, inserted by the walker a chunk behind (chunk k then sees chunks <= k - 4:
+// the repeats at 64..256 bytes that real files are full of were lost -- 6.6 % below the
+// reference's ratio on Python sources at round 5).  -8 % encode time.
+#ifndef APE_LZ4_ALLPOS
+#define APE_LZ4_ALLPOS 1
+#endif
+constexpr bool kAllPos = APE_LZ4_ALLPOS != 0;
 #ifndef APE_LZ4_TSIZE
 #define APE_LZ4_TSIZE 7200
 #endif
@@ -252,15 +270,20 @@ __device__ __forceinline__ void load32(gcu8 *in, int n, int pos, uint32_t (&X)[8
     }
 }
 
-// Hash of the 5 bytes at p (x1 = in[p..p+3], b4 = in[p+4]) into kHLog bits.  The
+// Hash of the kKey bytes at p (x0 = in[p..p+3], x1 = in[p+4..p+7]) onto [0, kHSize).  The
 // reference multiplies the 40-bit sequence by 889523592379 (:456-473), which needs
-// quarter-rate 32-bit multiplies here; any hash gives a valid stream, so this one
-// uses two full-rate 24 x 24-bit multiplies (v_mul_u32_u24) of bytes 0-2 and
-// bytes 3-4.  Same ratio on the App. C data (tools/enc_model.c: 3.1613 vs 3.1600).
-__device__ __forceinline__ uint32_t hash5(uint32_t x1, uint32_t b4) {
-    const uint32_t lo = x1 & 0xFFFFFFu, hi = (x1 >> 24) | ((b4 & 0xFFu) << 8);
-    // (__umul24 returns int: do the sum and the shift unsigned)
-    const uint32_t v = (uint32_t)__umul24(lo, 0x9E3779u) + (uint32_t)__umul24(hi, 0xC2B2AEu);
+// quarter-rate 32-bit multiplies here; any hash gives a valid stream, so this one uses
+// full-rate 24 x 24-bit multiplies (v_mul_u32_u24 / v_mad_u32_u24, which read only the low
+// 24 bits of their operands) of bytes 0-2 and 3-5 (and 6 or 6-7).  With kKey = 5 it is the
+// round-5 hash (same ratio as the reference's on App. C data, tools/enc_model.c).
+__device__ __forceinline__ uint32_t hashk(uint32_t x0, uint32_t x1) {
+    uint32_t hi;
+    if constexpr (kKey == 5) hi = (x0 >> 24) | ((x1 & 0xFFu) << 8);
+    else hi = __builtin_amdgcn_alignbyte(x1, x0, 3u);   // bytes 3..6 (the multiply takes 3..5)
+    // (__umul24 returns int: do the sums and the shift unsigned)
+    uint32_t v = (uint32_t)__umul24(x0, 0x9E3779u) + (uint32_t)__umul24(hi, 0xC2B2AEu);
+    if constexpr (kKey == 7) v += (uint32_t)__umul24((x1 >> 16) & 0xFFu, 0x27D4EBu);
+    if constexpr (kKey == 8) v += (uint32_t)__umul24(x1 >> 16, 0x27D4EBu);
     if constexpr (kHSize == (1 << kHLog)) return v >> (32 - kHLog);
     else return __umulhi(v, (uint32_t)kHSize);   // v scaled onto [0, kHSize): one v_mul_hi_u32
 }
@@ -476,7 +499,7 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     // (FAST: chunk k lies inside the block with room to spare, every lane is hashable)
     const bool hashable = FAST || (k < B.nch && p + 5u <= B.un);
-    h = hash5(X[0], X[1]);
+    h = hashk(X[0], X[1]);
     cT = S.tab[h];
     jL = 0xFFFFFFFFu;
     if (!B.noL) {   // wave-uniform
@@ -486,6 +509,11 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
         jL = hashable ? S.scr[hs] : 0xFFFFFFFFu;
         wave_sync();
         if (hashable) S.scr[hs] = 0xFFFFFFFFu;
+    }
+    if constexpr (kAllPos) {
+        // after this chunk's lookups (one wave's LDS operations complete in order); lanes with
+        // the same slot: the last lane's write lands last, the latest position wins
+        if (hashable) S.tab[h] = (uint16_t)p;
     }
     prod_fetch_t<SMALL, FAST>(B, k, lane, cT, Y);
 }
@@ -811,7 +839,7 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     // second half's hash needs no LDS round trip (the ring holds chunks k - 13 .. k + 2,
     // and a match the producer finished ends before p + 81; a match the walker extends
     // is hashed from the input instead)
-    O.e2v = ring8(S, P + (uint32_t)lane + O.Lf - 2u);
+    if constexpr (!kAllPos) O.e2v = ring8(S, P + (uint32_t)lane + O.Lf - 2u);
     if (W.q >= P + 64u) return;               // a match from earlier chunks covers it
     const uint2 iv = O.iv;
     const uint64_t Hm = wave_ballot(O.Lf != 0u);          // lanes with a match
@@ -877,7 +905,7 @@ __device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk 
     // walker extended is rehashed in walk_publish): independent of the scan below, so it
     // fills the scan's DPP wait states.  (No early exit for a chunk a match from earlier
     // chunks covers: it has no members, nothing is walked, the anchor stays.)
-    O.e2h = hash5(O.e2v.x, O.e2v.y);
+    if constexpr (!kAllPos) O.e2h = hashk(O.e2v.x, O.e2v.y);
     // catch-up limits: a member's backward extension stops at the previous end
     const uint32_t anchor0 = W.anchor;
     const bool mem = lane_in(O.members);
@@ -921,8 +949,9 @@ __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int
                                              const WalkOut &O, uint32_t &qn) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const uint2 iv = O.iv;
-    if (lane_in(O.walked) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
     const bool mem = lane_in(O.members);
+    if constexpr (!kAllPos) {   // (kAllPos: the producer has inserted every position)
+    if (lane_in(O.walked) && (iv.x & I_HASHABLE)) S.tab[iv.y >> 16] = (uint16_t)p;
     const uint32_t fwd = O.m_len - O.m_back;      // match length from p
     // match_end - 2 (:680) of the members, hashed here (off the producer's chain): from the
     // ring bytes read before the walk, or, for a match the walker extended, from the input
@@ -930,17 +959,16 @@ __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int
     const bool e2ok = mem && e2 + 5u <= B.un;
     uint32_t e2h = O.e2h;   // (ring bytes read before the walk: -1.6 % encode time)
     if (e2ok && (iv.x & I_TRUNC)) {   // rare: a match the walker extended
-        uint32_t lo32 = 0, b4 = 0;
-        for (uint32_t t = 0; t < 5u; t++) {
-            const uint32_t by = B.in[e2 + t];
-            if (t < 4) lo32 |= by << (8 * t); else b4 = by;
-        }
-        e2h = hash5(lo32, b4);
+        uint32_t w[2] = {0u, 0u};   // in[e2, e2 + 8), 0 past the block end (as A loads it)
+        for (uint32_t t = 0; t < 8u; t++)
+            if (e2 + t < B.un) w[t >> 2] |= (uint32_t)B.in[e2 + t] << (8 * (t & 3));
+        e2h = hashk(w[0], w[1]);
     }
     // one wave's LDS operations complete in order: the walked-position inserts above
     // land before these (compiler barrier only)
     __builtin_amdgcn_sched_barrier(0);
     if (e2ok) S.tab[e2h] = (uint16_t)e2;
+    }
     // the chunk's sequences, in order, as records for the emitter: literals from the
     // anchor to the match start (after catch-up), the match length and its offset
     if (mem) S.q[(qn + lane_rank(O.members)) & (kQ - 1u)] =
@@ -1160,7 +1188,7 @@ __device__ __forceinline__ void prefix_history(EncLds &S, const Blk &B, int lane
 #pragma unroll
         for (int u = 0; u < kU; u++) {
             const uint32_t v = v0 + 192u * u + 3u * (uint32_t)lane;
-            if (ok[u]) S.tab[hash5(x[u].x, x[u].y)] = (uint16_t)v;
+            if (ok[u]) S.tab[hashk(x[u].x, x[u].y)] = (uint16_t)v;
         }
     }
     const uint32_t p = D - 64u + (uint32_t)lane;
@@ -1437,19 +1465,8 @@ lz4_encode_kernel(BlockArgs a) {
     else encode_block<false, ACC>(S, B, wave, lane, &a.result[b]);
 }
 
-// compress_default (acceleration 1, no prefix) runs the segment-parallel encoder
-// (lz4_encode_seg.hip) when APE_LZ4_ENCODER=seg selects it (A/B until measured)
-static bool use_seg_encoder() {
-    static const int v = [] {
-        const char *e = getenv("APE_LZ4_ENCODER");
-        return (e && e[0] == 's') ? 1 : 0;
-    }();
-    return v != 0;
-}
-
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
-    if (a.accel <= 1 && !a.dict_size && use_seg_encoder()) return launch_encode_seg(a, s);
     if (a.accel > 1)
         hipLaunchKernelGGL(lz4_encode_kernel<true>, dim3(a.nblocks), dim3(192), 0, s, a);
     else

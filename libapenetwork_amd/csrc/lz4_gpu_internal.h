@@ -146,8 +146,6 @@ hipError_t launch_decode(const BlockArgs &a, bool partial, hipStream_t s);
 // workgroup per connection looping over its chunks in order (lz4_decode.hip)
 hipError_t launch_decode_chain(const BlockArgs &a, int nconn, int nq, hipStream_t s);
 hipError_t launch_encode(const BlockArgs &a, hipStream_t s);
-// the segment-parallel encoder (lz4_encode_seg.hip): acceleration 1, no prefix
-hipError_t launch_encode_seg(const BlockArgs &a, hipStream_t s);
 // the greedy-exact mode (lz4_encode_exact.hip): the reference's sequential parse, byte for byte
 hipError_t launch_encode_exact(const BlockArgs &a, hipStream_t s);
 // compress_destSize pass 2 (lz4_destsize.hip): scratch slot i (at scratch + i*stride, encoder

@@ -593,13 +593,11 @@ int APE_LZ4_synth_blocks_dev(char *d_out, size_t stride, int blockSize, long lon
 namespace apelz4 {
 hipError_t dec_stats_read(unsigned long long *out, int reset);
 hipError_t enc_stats_read(unsigned long long *out, int reset);
-hipError_t seg_stats_read(unsigned long long *out, int reset);
 }
 extern "C" {
 // Diagnostic build only: per-phase cycle sums (which: 0 = decode, 1 = encode).
 int APE_LZ4_debug_stats(int which, unsigned long long *out16, int reset) {
-    hipError_t e = which == 2 ? apelz4::seg_stats_read(out16, reset)
-                   : which ? apelz4::enc_stats_read(out16, reset) : apelz4::dec_stats_read(out16, reset);
+    hipError_t e = which ? apelz4::enc_stats_read(out16, reset) : apelz4::dec_stats_read(out16, reset);
     return e == hipSuccess ? 0 : -1;
 }
 #endif

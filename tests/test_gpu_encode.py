@@ -188,7 +188,7 @@ def test_block_limit(cuda, product):
     assert rs == [product.ERANGE]
 
 
-ACCEL_RATIO_TOL = 0.01   # |GPU / reference - 1| at acceleration 2, 4, 8 (measured -0.6..-0.8 %)
+ACCEL_RATIO_TOL = 0.01   # GPU >= (1 - tol) x reference at acceleration 1, 2, 4, 8
 
 
 def test_acceleration(cuda, product, oracle):
@@ -222,15 +222,10 @@ def test_acceleration(cuda, product, oracle):
     print("ratio by acceleration", {a: round(r, 4) for a, r in ratio.items()},
           "reference", {a: round(r, 4) for a, r in ref.items()})
     assert ratio[1] >= ratio[2] > ratio[4] > ratio[8] > ratio[1 << 30]
-    # acceleration 1 is compress_default: the opt-in segment encoder (four candidates per
-    # position) compresses better than the reference's single-candidate search; the default
-    # chunk encoder (7200-entry table) stays within the tolerance of the others
-    if os.environ.get("APE_LZ4_ENCODER", "").startswith("s"):
-        assert ratio[1] >= ref[1]
-    else:
-        assert abs(ratio[1] / ref[1] - 1.0) <= ACCEL_RATIO_TOL, (1, ratio[1], ref[1])
-    for a in (2, 4, 8):
-        assert abs(ratio[a] / ref[a] - 1.0) <= ACCEL_RATIO_TOL, (a, ratio[a], ref[a])
+    # one-sided: the GPU's 6-byte key and near candidate compress App. C data better than
+    # the reference's search (round 6: +7 % at a = 1); a ratio 1 % below the reference's fails
+    for a in (1, 2, 4, 8):
+        assert ratio[a] >= (1.0 - ACCEL_RATIO_TOL) * ref[a], (a, ratio[a], ref[a])
     # a huge acceleration probes only the three positions after each match end (and the
     # block's first three): little is found, but the blocks stay valid (checked above)
     assert ratio[1 << 30] < 1.5

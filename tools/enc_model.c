@@ -290,11 +290,170 @@ static long model4(const uint8_t *in, int n, int lag, int pol, int sb, int lmax)
     return out;
 }
 
+
+/* Round 6: key length and T-probe density.  The product policy of
+ * model4 (pol 7, lag 3, 6 in-chunk bits, catch-up <= 4, table scaled onto g_tsize entries by
+ * v_mul_hi_u32 as lz4_encode.hip does) with the hash over `key` bytes (5..8, the GPU's
+ * two / three full-rate 24-bit multiplies) and the table candidate T probed only at
+ * positions p % tmod == 0 (every walked position is still inserted; L everywhere).
+ * Returns the compressed size, adds the block's sequence count to *nseq. */
+static uint32_t hkey(const uint8_t *p, int key) {
+    uint32_t x0 = rd32(p), x1 = rd32(p + 4);
+    uint32_t lo = x0 & 0xFFFFFF, hi = (x0 >> 24) | (x1 << 8);
+    if (key == 5) hi &= 0xFFFF;
+    hi &= 0xFFFFFF;
+    uint32_t v = lo * 0x9E3779u + hi * 0xC2B2AEu;
+    if (key == 7) v += (x1 >> 16 & 0xFF) * 0x27D4EBu;         /* byte 6 */
+    if (key == 8) v += (x1 >> 16) * 0x27D4EBu;                 /* bytes 6-7 */
+    return v;
+}
+static uint32_t kslot(const uint8_t *p, int key) {
+    return (uint32_t)(((uint64_t)hkey(p, key) * (uint32_t)g_tsize) >> 32);
+}
+static int g_lag = 3, g_bcap = 4, g_noL = 0, g_near = 0, g_nearbits = 6, g_nearwin = 768, g_allins = 0;
+static long model5(const uint8_t *in, int n, int key, int tmod, long *nseq)
+{
+    int tab[8192], near[1024];
+    for (int i = 0; i < 8192; i++) tab[i] = -1;
+    for (int i = 0; i < 1024; i++) near[i] = -1;
+    int *cT = malloc(4 * n), *cL = malloc(4 * n), scr[64];
+    int *ins = malloc(8 * n), *insc = malloc(8 * n), nins = 0, done = 0;
+    const int lag = g_lag, mstart = n - 12, mlimit = n - 5, nch = (n + 63) / 64;
+    long out = 0;
+    int anchor = 0, p = 0;
+    for (int k = 0; k < nch; k++) {
+        while (done < nins && insc[done] <= k - lag - 1) {
+            int q = ins[done++];
+            if (q + 8 <= n) tab[kslot(in + q, key)] = q;
+        }
+        int r0 = 64 * k, r1 = r0 + 64 < n ? r0 + 64 : n;
+        for (int i = 0; i < 64; i++) scr[i] = -1;
+        for (int q = r0; q < r1; q++) {
+            uint32_t h = q + 8 <= n ? kslot(in + q, key) : 0;
+            cT[q] = (q % tmod == 0) ? tab[h] : -1;
+            cL[q] = -1;
+            if (g_near == 2) {
+                /* one ds_max_rtn per lane on ((k+1) << 6 | 63 - lane) over 2^nearbits buckets,
+                 * lanes in order: the first lane of a bucket gets the earliest lane of the last
+                 * earlier chunk that had it, later lanes the earliest lane of this chunk */
+                const int nb = h & ((1 << g_nearbits) - 1);
+                const int r = near[nb] < 0 ? 0 : near[nb];
+                const int w = ((k + 1) << 6) | (63 - (q - r0));
+                if (w > r) near[nb] = w;
+                const int c = 64 * (r >> 6) - 1 - (r & 63);
+                if (r && q - c <= g_nearwin && (!g_noL || (r >> 6) != k + 1)) cL[q] = c;
+                continue;
+            }
+            if (scr[h & 63] < 0) {
+                scr[h & 63] = q;
+                /* near: the latest position of the earlier chunks with the same low bits */
+                const int nb = h & ((1 << g_nearbits) - 1);
+                if (g_near && near[nb] >= 0 && q - near[nb] <= g_nearwin) cL[q] = near[nb];
+            } else if (!g_noL) cL[q] = scr[h & 63];
+        }
+        if (g_near == 1)
+            for (int q = r0; q < r1; q++) if (q + 8 <= n) near[kslot(in + q, key) & ((1 << g_nearbits) - 1)] = q;
+        if (g_allins)   /* the producer inserts every position of the chunk after its lookups */
+            for (int q = r0; q < r1; q++) if (q + 8 <= n) tab[kslot(in + q, key)] = q;
+        while (p < r1) {
+            int best = 0, bc = -1;
+            if (p >= 1 && p <= mstart) {
+                int cs[2] = {cT[p], cL[p]}, ok[2], l[2] = {0, 0};
+                for (int j = 0; j < 2; j++) {
+                    int c = cs[j];
+                    ok[j] = !(c < 0 || c >= p || p - c > 65535) && rd32(in + c) == rd32(in + p);
+                    if (ok[j]) { l[j] = 4; while (p + l[j] < mlimit && in[p + l[j]] == in[c + l[j]]) l[j]++; }
+                }
+                int pick = -1, l12 = l[1] < 12 ? l[1] : 12;
+                if (ok[1] && (!ok[0] || (l[0] < 12 && l12 >= l[0]))) pick = 1;
+                else if (ok[0]) pick = 0;
+                if (pick >= 0) { best = l[pick]; bc = cs[pick]; }
+            }
+            if (!g_allins) { ins[nins] = p; insc[nins++] = k; }
+            if (best >= 4) {
+                int m = p, c = bc, len = best, b = 0;
+                while (b < g_bcap && m > anchor && c > 0 && in[m - 1] == in[c - 1]) { m--; c--; len++; b++; }
+                int lit = m - anchor;
+                out += 1 + ext(lit) + lit + 2 + ext(len - 4);
+                (*nseq)++;
+                p = m + len;
+                anchor = p;
+                if (!g_allins) { ins[nins] = p - 2; insc[nins++] = (p - 2) / 64 > k ? (p - 2) / 64 : k; }
+            } else p++;
+        }
+    }
+    out += 1 + ext(n - anchor) + n - anchor;
+    free(cT); free(cL); free(ins); free(insc);
+    return out;
+}
+
+static void key_study(const uint8_t *buf, int n, int nb, const char *what)
+{
+    if (getenv("LAGSTUDY")) {
+        struct { int lag, bcap, ts, noL; } V[] = {{3,4,7200,0},{0,4,7200,0},{3,1000,7200,0},{3,4,8192,0},
+            {0,1000,8192,0},{3,4,7200,1},{1,4,7200,0},{2,4,7200,0}};
+        for (unsigned i = 0; i < sizeof(V)/sizeof(V[0]); i++) {
+            g_lag = V[i].lag; g_bcap = V[i].bcap; g_tsize = V[i].ts; g_noL = V[i].noL;
+            long tot = 0, nseq = 0;
+            for (int b = 0; b < nb; b++) tot += model5(buf + (size_t)b * n, n, 5, 1, &nseq);
+            printf("%-5s lag %d bcap %4d table %d noL %d  ratio %.4f  seq %7.1f\n", what, g_lag, g_bcap,
+                   g_tsize, g_noL, (double)n * nb / tot, (double)nseq / nb);
+        }
+        g_lag = 3; g_bcap = 4; g_noL = 0;
+    }
+    g_tsize = getenv("TSIZE") ? atoi(getenv("TSIZE")) : 7200;
+    if (getenv("ALLINS")) {
+        for (int key = 5; key <= 7; key++)
+            for (int ai = 0; ai < 2; ai++) {
+                g_allins = ai;
+                long tot = 0, nseq = 0;
+                for (int b = 0; b < nb; b++) tot += model5(buf + (size_t)b * n, n, key, 1, &nseq);
+                printf("%-5s key %d all-positions %d  ratio %.4f  seq %7.1f\n", what, key, ai,
+                       (double)n * nb / tot, (double)nseq / nb);
+            }
+        g_allins = 0;
+        return;
+    }
+    if (getenv("NEAR")) {
+        const int nbits[] = {6, 7, 8};
+        const int tm = atoi(getenv("NEAR"));
+        const int mode = getenv("NEARMODE") ? atoi(getenv("NEARMODE")) : 1;
+        for (int key = 5; key <= 8; key++)
+            for (int i = -1; i < 3; i++) {
+                g_near = i >= 0 ? mode : 0; g_nearbits = i >= 0 ? nbits[i] : 6;
+                long tot = 0, nseq = 0;
+                for (int b = 0; b < nb; b++) tot += model5(buf + (size_t)b * n, n, key, tm, &nseq);
+                printf("%-5s key %d T every %d near %d bits %2d  ratio %.4f  seq %7.1f\n", what, key, tm, g_near,
+                       g_nearbits, (double)n * nb / tot, (double)nseq / nb);
+            }
+        g_near = 0;
+        return;
+    }
+    for (int tmod = 1; tmod <= 2; tmod++)
+        for (int key = 5; key <= 8; key++) {
+            long tot = 0, nseq = 0;
+            for (int b = 0; b < nb; b++) tot += model5(buf + (size_t)b * n, n, key, tmod, &nseq);
+            printf("%-5s key %d  T every %d  ratio %.4f  sequences/block %7.1f\n", what, key, tmod,
+                   (double)n * nb / tot, (double)nseq / nb);
+        }
+    g_tsize = 8192;
+}
+
 int main(int argc, char **argv)
 {
     const int n = 65536, nb = argc > 1 ? atoi(argv[1]) : 16;
     uint8_t *buf = malloc((size_t)n * nb + 16);
     synth_blocks(buf, n, n, 0, nb, 1);
+    if (argc > 2) {   /* key study: App. C blocks, then the blocks of file argv[2] */
+        key_study(buf, n, nb, "appC");
+        FILE *f = fopen(argv[2], "rb");
+        if (!f) return 1;
+        const int nt = (int)fread(buf, 1, (size_t)n * nb, f) / n;
+        fclose(f);
+        key_study(buf, n, nt, "file");
+        free(buf);
+        return 0;
+    }
     struct { int hlog, insert, R, inround, back; const char *name; } P[] = {
         {12, 0, 2048, 1, 0, "current: 4096, all positions, 2048 rounds, in-round"},
         {13, 0, 2048, 1, 0, "8192, all positions, 2048 rounds, in-round"},
