@@ -1,5 +1,5 @@
 #!/bin/bash
-# Copy a tools/gpu_r5_refresh.sh run's results from gpurun_out/ into profiles/ (run here).
+# Copy a tools/gpu_refresh.sh run's results from gpurun_out/ into profiles/ (run here).
 set -e
 TAG=${1:-r2}
 cd "$(dirname "$0")/.."

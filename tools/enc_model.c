@@ -310,10 +310,10 @@ static uint32_t hkey(const uint8_t *p, int key) {
 static uint32_t kslot(const uint8_t *p, int key) {
     return (uint32_t)(((uint64_t)hkey(p, key) * (uint32_t)g_tsize) >> 32);
 }
-static int g_lag = 3, g_bcap = 4, g_noL = 0, g_near = 0, g_nearbits = 6, g_nearwin = 768, g_allins = 0;
+static int g_lag = 3, g_bcap = 4, g_noL = 0, g_near = 0, g_nearbits = 6, g_nearwin = 768, g_allins = 0, g_insd = 0;
 static long model5(const uint8_t *in, int n, int key, int tmod, long *nseq)
 {
-    int tab[8192], near[1024];
+    int tab[8192], near[1024], tabold[64];
     for (int i = 0; i < 8192; i++) tab[i] = -1;
     for (int i = 0; i < 1024; i++) near[i] = -1;
     int *cT = malloc(4 * n), *cL = malloc(4 * n), scr[64];
@@ -331,6 +331,7 @@ static long model5(const uint8_t *in, int n, int key, int tmod, long *nseq)
         for (int q = r0; q < r1; q++) {
             uint32_t h = q + 8 <= n ? kslot(in + q, key) : 0;
             cT[q] = (q % tmod == 0) ? tab[h] : -1;
+            tabold[q - r0] = tab[h];
             cL[q] = -1;
             if (g_near == 2) {
                 /* one ds_max_rtn per lane on ((k+1) << 6 | 63 - lane) over 2^nearbits buckets,
@@ -353,8 +354,15 @@ static long model5(const uint8_t *in, int n, int key, int tmod, long *nseq)
         }
         if (g_near == 1)
             for (int q = r0; q < r1; q++) if (q + 8 <= n) near[kslot(in + q, key) & ((1 << g_nearbits) - 1)] = q;
-        if (g_allins)   /* the producer inserts every position of the chunk after its lookups */
-            for (int q = r0; q < r1; q++) if (q + 8 <= n) tab[kslot(in + q, key)] = q;
+        if (g_allins)   /* the producer inserts every position of the chunk after its lookups
+                           (only over entries more than g_insd bytes back: the value the lane
+                           read, so lanes of one chunk decide on the same old entry) */
+            for (int q = r0; q < r1; q++) {
+                if (q + 8 > n) continue;
+                const uint32_t h = kslot(in + q, key);
+                const int old = tabold[q - r0];
+                if (old < 0 || q - old > g_insd) tab[h] = q;
+            }
         while (p < r1) {
             int best = 0, bc = -1;
             if (p >= 1 && p <= mstart) {
@@ -403,12 +411,13 @@ static void key_study(const uint8_t *buf, int n, int nb, const char *what)
     }
     g_tsize = getenv("TSIZE") ? atoi(getenv("TSIZE")) : 7200;
     if (getenv("ALLINS")) {
-        for (int key = 5; key <= 7; key++)
-            for (int ai = 0; ai < 2; ai++) {
-                g_allins = ai;
+        const int ds[] = {0, 0, 256, 1024, 4096, 16384, 1 << 20};
+        for (int key = 6; key <= 8; key++)
+            for (int ai = 0; ai < 7; ai++) {
+                g_allins = ai > 0; g_insd = ds[ai];
                 long tot = 0, nseq = 0;
                 for (int b = 0; b < nb; b++) tot += model5(buf + (size_t)b * n, n, key, 1, &nseq);
-                printf("%-5s key %d all-positions %d  ratio %.4f  seq %7.1f\n", what, key, ai,
+                printf("%-5s key %d all-positions %d  dist %7d  ratio %.4f  seq %7.1f\n", what, key, g_allins, g_insd,
                        (double)n * nb / tot, (double)nseq / nb);
             }
         g_allins = 0;

@@ -1,19 +1,19 @@
 #!/bin/bash
-# Round-5 profile refresh at a commit (GPU box), in two calls that each fit gpurun's limit.
-# Results land under gpurun_out/; tools/collect_profiles.sh r5 copies the common ones into
+# Profile refresh at a commit (GPU box), in two calls that each fit gpurun's limit.
+# Results land under gpurun_out/; tools/collect_profiles.sh TAG copies the common ones into
 # profiles/.
 #   part A: GPU parity suite + smoke, the bench line + rocprofv3 kernel stats of the same
 #           command, SQ issue passes, PMC traffic passes (FETCH_SIZE, WRITE_SIZE, requests)
 #   part B: memory-pipeline passes (TA/TD busy), phase timers, config 2 (rocprofv3 kernel
 #           time + FETCH_SIZE / WRITE_SIZE passes of bench.py --rand4k), --stream, --e2e,
 #           --sock-chained
-#   usage: bash tools/gpu_r5_refresh.sh A|B [TAG]
+#   usage: bash tools/gpu_refresh.sh A|B [TAG]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 PART=${1:-A}
-TAG=${2:-r5}
+TAG=${2:-r6}
 if [ "$PART" = A ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -20 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
   tail -2 gpurun_out/pytest_gpu_$TAG.log

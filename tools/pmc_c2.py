@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """pmc_c2.py -- DESIGN TOOL: config 2's decode kernel HBM bytes per launch from the
 rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py --rand4k --steps 1 --warmup 0`
-(tools/gpu_r5_refresh.sh B) next to its algorithmic bytes and rocprofv3 kernel time.
+(tools/gpu_refresh.sh B) next to its algorithmic bytes and rocprofv3 kernel time.
 FETCH_SIZE is corrected x2 (profiles/fetch_calib.json: every request counts 64 B on gfx950,
 the codec's requests are 128 B); WRITE_SIZE as reported.  KB = 1024 B.
   python3 tools/pmc_c2.py TAG   -> profiles/TAG_config2_pmc.json"""
