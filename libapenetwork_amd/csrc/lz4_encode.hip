@@ -90,8 +90,21 @@ static_assert(kKey >= 5 && kKey <= 8, "hash key of 5..8 bytes");
 #define APE_LZ4_ALLPOS 1
 #endif
 constexpr bool kAllPos = APE_LZ4_ALLPOS != 0;
+// The in-chunk candidate L (the earliest lane of the chunk with the same 6 hash bits; an LDS
+// scratch, 4 ds_bpermute, a 12-byte measure and the pick): 1 = none.  With every position in
+// the table (kAllPos) T finds the repeats from earlier chunks at no lag, so L only adds a
+// first repeat inside one chunk: without it encode -8.7 %, decode -2.5 %, ratio -0.7 % on App.
+// C data and -1.3 % on real files (profiles/r6_encoder_policy_ab.txt).  Its scratch's 256 bytes
+// go to the table: 7328 entries.
+#ifndef APE_LZ4_NOL
+#define APE_LZ4_NOL 1
+#endif
 #ifndef APE_LZ4_TSIZE
+#if APE_LZ4_NOL
+#define APE_LZ4_TSIZE 7328
+#else
 #define APE_LZ4_TSIZE 7200
+#endif
 #endif
 constexpr int kHSize = APE_LZ4_TSIZE;
 static_assert(kHSize <= (1 << kHLog) && kHSize % 8 == 0, "table size");
@@ -105,7 +118,8 @@ static_assert(kHSize <= (1 << kHLog) && kHSize % 8 == 0, "table size");
 #define APE_LZ4_EAGER_T 12
 #endif
 constexpr uint32_t kEagerLen = APE_LZ4_EAGER_T;   // match bytes measured by C1 (T candidate)
-static_assert(kEagerLen == 12 || kEagerLen == 16 || kEagerLen == 20, "C1 measures T to 12, 16 or 20 bytes");
+static_assert(kEagerLen == 8 || kEagerLen == 12 || kEagerLen == 16 || kEagerLen == 20,
+              "C1 measures T to 8, 12, 16 or 20 bytes");
 constexpr int kYW = (int)(kEagerLen + 4u) / 4;   // T-candidate dwords loaded: in[T-4, T+kEagerLen)
 constexpr uint32_t kEagerL = 12;     // ... for the in-chunk candidate L
 // Stage 2 (C2) measures only the candidates C1 left truncated (~13 % of the lanes on App.
@@ -126,7 +140,7 @@ static_assert(kRingE < 65536u, "the ring holds recent input, not the block's win
 #ifndef APE_LZ4_SCRBITS
 #define APE_LZ4_SCRBITS 6
 #endif
-constexpr uint32_t kScr = 1u << APE_LZ4_SCRBITS;  // in-chunk candidate scratch entries
+[[maybe_unused]] constexpr uint32_t kScr = 1u << APE_LZ4_SCRBITS;  // in-chunk candidate scratch
 constexpr int kSmall = 128;          // smaller blocks take the byte-load path
 // Sequence records in flight between the walker and the emitter.  The emitter reads up to
 // 64 records into registers at a fetch (its slots are free from then on); it fetches when
@@ -147,6 +161,7 @@ static_assert(kFetchAt < kEmitAll, "a fetch precedes emit_all");
 #ifndef APE_LZ4_ACC_L
 #define APE_LZ4_ACC_L 1
 #endif
+constexpr bool kNoL = APE_LZ4_NOL != 0;
 #ifndef APE_LZ4_APF
 #define APE_LZ4_APF 1                // producer: own-bytes load A two steps ahead (else one)
 #endif
@@ -175,7 +190,9 @@ struct __attribute__((aligned(16))) EncLds {
     uint2 info[64];                  // producer -> walker: chunk k, written in the second half of
                                      // step k, read at the start of step k + 1 (before the
                                      // producer writes chunk k + 1 after the mid barrier)
+#if !APE_LZ4_NOL
     uint32_t scr[kScr];              // producer scratch: earliest lane per low hash bits
+#endif
     uint2 q[kQ];                     // walker -> emitter: sequence records, record r in
                                      // [r % kQ]: {lit | (match length - 4) << 16, offset}
     uint32_t qn;                     // walker -> emitter: records published
@@ -382,8 +399,13 @@ __device__ __forceinline__ uint2 ring8(const EncLds &S, uint32_t x) {
 template <int NW, int NA>
 __device__ __forceinline__ void loadv(gcu8 *in, uint32_t un, uint32_t pos, uint32_t (&X)[NA],
                                       bool fast) {
-    static_assert(NW >= 4 && NW <= 6 && NW <= NA, "loadv");
+    static_assert(NW >= 3 && NW <= 6 && NW <= NA, "loadv");
     if (fast) {
+        if constexpr (NW == 3) {
+            const uint3 a = gload12(in + pos);
+            X[0] = a.x; X[1] = a.y; X[2] = a.z;
+            return;
+        }
         const uint4 a = gload16(in + pos);
         X[0] = a.x; X[1] = a.y; X[2] = a.z; X[3] = a.w;
         if constexpr (NW == 6) {
@@ -502,13 +524,15 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
     h = hashk(X[0], X[1]);
     cT = S.tab[h];
     jL = 0xFFFFFFFFu;
-    if (!B.noL) {   // wave-uniform
+    if (!kNoL && !B.noL) {   // wave-uniform
+#if !APE_LZ4_NOL
         const uint32_t hs = h & (kScr - 1u);
         if (hashable) atomicMin(&S.scr[hs], (uint32_t)lane);
         wave_sync();
         jL = hashable ? S.scr[hs] : 0xFFFFFFFFu;
         wave_sync();
         if (hashable) S.scr[hs] = 0xFFFFFFFFu;
+#endif
     }
     if constexpr (kAllPos) {
         // after this chunk's lookups (one wave's LDS operations complete in order); lanes with
@@ -609,7 +633,7 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
     const bool okT = can & (cT < p) & (cT >= 4u) & (Y[1] == X[1]);
     // (no cL != cT test: when L's candidate is T's, L is kept only when T < 12 bytes, and then
     // both give the same position, length and preceding bytes)
-    const bool okL = can & (jL < (uint32_t)lane) & (Z[1] == X[1]);   // jL = ~0 if noL
+    const bool okL = !kNoL && (can & (jL < (uint32_t)lane) & (Z[1] == X[1]));   // jL = ~0 if noL
     // (FAST: the match limit lies >= 132 bytes past every lane, beyond anything C1 and C2
     // measure, so it never cuts a length: no limit arithmetic at all)
     R.lim = FAST ? 0xFFFFu : (can ? B.mlimit - p : 0u);   // (a FAST chunk finished by a
@@ -1457,7 +1481,9 @@ lz4_encode_kernel(BlockArgs a) {
 
     // table = 0 (the reference's memset state: position 0 for every hash)
     for (int i = tid; i < kHSize / 8; i += 192) ((uint4 *)S.tab)[i] = make_uint4(0, 0, 0, 0);
+#if !APE_LZ4_NOL
     for (int i = tid; i < (int)kScr; i += 192) S.scr[i] = 0xFFFFFFFFu;
+#endif
     for (int i = tid; i < (int)(kRingE / 16 + 4); i += 192) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
     if (tid == 0) S.qn = 0u;
     __syncthreads();

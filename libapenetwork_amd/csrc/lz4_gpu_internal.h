@@ -27,6 +27,11 @@ __device__ __forceinline__ uint4 gload16(gcu8 *p) {
     const u32x4_u v = *(__attribute__((address_space(1))) const u32x4_u *)p;
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+typedef uint32_t u32x3_u __attribute__((ext_vector_type(3), aligned(1)));
+__device__ __forceinline__ uint3 gload12(gcu8 *p) {
+    const u32x3_u v = *(__attribute__((address_space(1))) const u32x3_u *)p;
+    return make_uint3(v.x, v.y, v.z);
+}
 __device__ __forceinline__ uint2 gload8(gcu8 *p) {
     const u32x2_u v = *(__attribute__((address_space(1))) const u32x2_u *)p;
     return make_uint2(v.x, v.y);

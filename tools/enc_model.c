@@ -412,8 +412,11 @@ static void key_study(const uint8_t *buf, int n, int nb, const char *what)
     g_tsize = getenv("TSIZE") ? atoi(getenv("TSIZE")) : 7200;
     if (getenv("ALLINS")) {
         const int ds[] = {0, 0, 256, 1024, 4096, 16384, 1 << 20};
+        const int nv = getenv("ALLINS")[0] == '2' ? 2 : 7;
+        g_noL = getenv("NOL") ? 1 : 0;
+        g_bcap = getenv("BCAP") ? atoi(getenv("BCAP")) : 4;
         for (int key = 6; key <= 8; key++)
-            for (int ai = 0; ai < 7; ai++) {
+            for (int ai = 0; ai < nv; ai++) {
                 g_allins = ai > 0; g_insd = ds[ai];
                 long tot = 0, nseq = 0;
                 for (int b = 0; b < nb; b++) tot += model5(buf + (size_t)b * n, n, key, 1, &nseq);
