@@ -251,7 +251,9 @@ long long APE_LZ4_socket_recv_blocks(int fd, char *h_dst, size_t dst_stride, int
  *                        h_out + (m * nconn + i) * out_stride.  h_status[i] = 0 or the first
  *                        bad result of connection i.  Returns the payload bytes or
  *                        APE_LZ4_GPU_E* (EINVAL: malformed frame, early EOF, failed decode).
- * One thread may send while another receives on the same chain. */
+ * One thread may send while another receives on the same chain.  Errors are sticky per
+ * direction: a failed call has consumed frames / advanced the streams it ran, so every later
+ * call in that direction returns APE_LZ4_GPU_EINVAL (h_status[i] = -1); free the chain. */
 typedef struct APE_LZ4_chain APE_LZ4_chain;
 APE_LZ4_chain *APE_LZ4_chain_new(int nconn, int msg_len);
 void APE_LZ4_chain_free(APE_LZ4_chain *c);

@@ -567,6 +567,10 @@ struct ChainPart {
     // the messages one call needs, and the next call on the chain resumes with those bytes
     std::vector<APE_LZ4_rxbuf *> rb;
     std::vector<char> eof;
+    // sticky failure: a failed call has consumed frames and advanced the stream
+    // position / history of its direction for the rounds it ran, so no later call in that
+    // direction can be correct -- each returns APE_LZ4_GPU_EINVAL until the chain is freed
+    bool tx_failed = false, rx_failed = false;
 };
 
 namespace {
@@ -668,6 +672,7 @@ ChainPart *part_new(int nconn, int msg_len, int dev) {
 // Returns the bytes written or an error code.
 long long part_send(ChainPart *c, const int *fds, const char *h_msgs, size_t msg_stride,
                     size_t row_pitch, int nmsg) {
+    if (c->tx_failed) return APE_LZ4_GPU_EINVAL;
     if (hipSetDevice(c->dev) != hipSuccess) return APE_LZ4_GPU_ENODEV;
     const int M = c->nconn, nch = c->nch, nr = (nmsg + c->K - 1) / c->K;
     long long sent = 0;
@@ -728,6 +733,7 @@ long long part_send(ChainPart *c, const int *fds, const char *h_msgs, size_t msg
     }
     if (hipStreamSynchronize(c->tst) != hipSuccess && rc == 0) rc = APE_LZ4_GPU_ELAUNCH;
     sock_add(6, now_ns() - t_all);
+    if (rc) c->tx_failed = true;
     return rc ? rc : sent;
 }
 
@@ -738,6 +744,10 @@ long long part_send(ChainPart *c, const int *fds, const char *h_msgs, size_t msg
 // an error code (EINVAL also for a malformed frame or an early EOF).
 long long part_recv(ChainPart *c, const int *fds, char *h_out, size_t out_stride, size_t row_pitch,
                     int nmsg, int *h_status) {
+    if (c->rx_failed) {
+        for (int i = 0; i < c->nconn; i++) h_status[i] = -1;
+        return APE_LZ4_GPU_EINVAL;
+    }
     if (hipSetDevice(c->dev) != hipSuccess) return APE_LZ4_GPU_ENODEV;
     const int M = c->nconn, nch = c->nch, nr = (nmsg + c->K - 1) / c->K;
     const int maxf = c->K * nch;   // frames of a full round per connection
@@ -917,6 +927,7 @@ long long part_recv(ChainPart *c, const int *fds, char *h_out, size_t out_stride
     // became busy: nothing of this call is in flight when it returns
     if (hipStreamSynchronize(c->rst) != hipSuccess && rc == 0) rc = APE_LZ4_GPU_ELAUNCH;
     sock_add(7, now_ns() - t_all);
+    if (rc) c->rx_failed = true;
     return rc ? rc : got;
 }
 

@@ -481,6 +481,50 @@ def test_chain_recv_resumes_across_calls(cuda, product, monkeypatch, split, per_
         r.close()
 
 
+@pytest.mark.gpu
+def test_chain_errors_are_sticky(cuda, product):
+    """a failed recv has consumed frames and advanced the streams, so the chain must
+    not resume after it.  Message 1 of connection 0 carries a frame whose size field is past the
+    bound (malformed): the call that reaches it fails, and so does every later recv on the chain
+    (status -1), though the bytes after it are intact."""
+    nconn, msg_len, nmsg = 2, 65536, 4
+    peer = _ref_peer()
+    msgs = _chain_msgs(cuda, product, nmsg, nconn, msg_len, seed=7)
+    streams = [bytearray(_ref_tx(peer, [msgs[m, i].tobytes() for m in range(nmsg)]))
+               for i in range(nconn)]
+    at, nfr = 0, 0
+    while nfr < msg_len // 8192:   # skip message 0's frames of connection 0
+        at += 4 + int.from_bytes(streams[0][at:at + 4], "little")
+        nfr += 1
+    streams[0][at:at + 4] = (1 << 20).to_bytes(4, "little")
+    pairs = [_pair() for _ in range(nconn)]
+
+    def txf(i):
+        pairs[i][0].sendall(bytes(streams[i]))
+        pairs[i][0].shutdown(socket.SHUT_WR)
+
+    ths = [threading.Thread(target=txf, args=(i,)) for i in range(nconn)]
+    for t in ths:
+        t.start()
+    ch = product.Chain(nconn, msg_len)
+    fds = [r.fileno() for _, r in pairs]
+    out = np.zeros((1, nconn, msg_len), dtype=np.uint8)
+    status = np.full(nconn, -9, dtype=np.int32)
+    assert ch.recv(fds, out, status) == nconn * msg_len and (status == 0).all()
+    assert np.array_equal(out, msgs[0:1])
+    for _ in range(2):   # the failing call, then a later one: both raise
+        status[:] = -9
+        with pytest.raises(product.GpuError):
+            ch.recv(fds, out, status)
+    assert (status == -1).all()
+    ch.free()
+    for t in ths:
+        t.join()
+    for t, r in pairs:
+        t.close()
+        r.close()
+
+
 def test_chain_argument_checks(product):
     """Chain.send/recv check the array shapes, dtypes and strides the C side
     assumes (one row pitch = nconn x strides[1]; int32 status of length nconn)."""
