@@ -939,6 +939,9 @@ constexpr int kChainThreads = 8;
 
 struct APE_LZ4_chain {
     int nconn = 0, msg = 0, nparts = 0;
+    // sticky per direction over the whole chain: the parts that did not fail advanced their
+    // streams in the failed call, so no connection of it can resume either
+    bool tx_failed = false, rx_failed = false;
     int first[kChainThreads + 1] = {};
     ChainPart *part[kChainThreads] = {};
 };
@@ -1000,11 +1003,14 @@ void APE_LZ4_chain_free(APE_LZ4_chain *c) {
 long long APE_LZ4_chain_send(APE_LZ4_chain *c, const int *fds, const char *h_msgs,
                              size_t msg_stride, int nmsg) {
     if (!c || !fds || !h_msgs || nmsg < 0 || msg_stride < (size_t)c->msg) return APE_LZ4_GPU_EINVAL;
-    return chain_parallel(c, [&](int p) {
+    if (c->tx_failed) return APE_LZ4_GPU_EINVAL;
+    const long long r = chain_parallel(c, [&](int p) {
         const int i0 = c->first[p];
         return part_send(c->part[p], fds + i0, h_msgs + (size_t)i0 * msg_stride, msg_stride,
                          (size_t)c->nconn * msg_stride, nmsg);
     });
+    if (r < 0) c->tx_failed = true;
+    return r;
 }
 
 // RX: nmsg messages per connection; message m of connection i is decoded into h_out + (m *
@@ -1013,11 +1019,17 @@ long long APE_LZ4_chain_recv(APE_LZ4_chain *c, const int *fds, char *h_out, size
                              int nmsg, int *h_status) {
     if (!c || !fds || !h_out || !h_status || nmsg < 0 || out_stride < (size_t)c->msg)
         return APE_LZ4_GPU_EINVAL;
-    return chain_parallel(c, [&](int p) {
+    if (c->rx_failed) {
+        for (int i = 0; i < c->nconn; i++) h_status[i] = -1;
+        return APE_LZ4_GPU_EINVAL;
+    }
+    const long long r = chain_parallel(c, [&](int p) {
         const int i0 = c->first[p];
         return part_recv(c->part[p], fds + i0, h_out + (size_t)i0 * out_stride, out_stride,
                          (size_t)c->nconn * out_stride, nmsg, h_status + i0);
     });
+    if (r < 0) c->rx_failed = true;
+    return r;
 }
 
 }  // extern "C"

@@ -419,7 +419,8 @@ static void key_study(const uint8_t *buf, int n, int nb, const char *what)
             for (int ai = 0; ai < nv; ai++) {
                 g_allins = ai > 0; g_insd = ds[ai];
                 long tot = 0, nseq = 0;
-                for (int b = 0; b < nb; b++) tot += model5(buf + (size_t)b * n, n, key, 1, &nseq);
+                const int tm = getenv("TMOD") ? atoi(getenv("TMOD")) : 1;
+                for (int b = 0; b < nb; b++) tot += model5(buf + (size_t)b * n, n, key, tm, &nseq);
                 printf("%-5s key %d all-positions %d  dist %7d  ratio %.4f  seq %7.1f\n", what, key, g_allins, g_insd,
                        (double)n * nb / tot, (double)nseq / nb);
             }
