@@ -90,6 +90,19 @@ static_assert(kKey >= 5 && kKey <= 8, "hash key of 5..8 bytes");
 #define APE_LZ4_ALLPOS 1
 #endif
 constexpr bool kAllPos = APE_LZ4_ALLPOS != 0;
+// One workgroup barrier per step instead of two (1).  The mid-step barrier orders the walker's
+// table inserts after the producer's lookups and the walker's read of the single info array
+// before the producer's next write; with kAllPos the walker inserts nothing, and the info array
+// can be double-buffered by chunk parity (its 512 bytes from the table), so each role runs its
+// whole step and the three meet once.  Measured: encode time unchanged (44.07 vs 44.06 ms per
+// 131072 blocks; the texture path and VALU issue, not the barriers, set the step), ratio
+// -0.24 % from the smaller table -- off
+#ifndef APE_LZ4_ONEBAR
+#define APE_LZ4_ONEBAR 0
+#endif
+constexpr bool kOneBar = APE_LZ4_ONEBAR != 0;
+static_assert(!kOneBar || kAllPos, "one barrier per step needs the producer-only table");
+constexpr uint32_t kInfoBufs = kOneBar ? 2u : 1u;
 // The in-chunk candidate L (the earliest lane of the chunk with the same 6 hash bits; an LDS
 // scratch, 4 ds_bpermute, a 12-byte measure and the pick): 1 = none.  With every position in
 // the table (kAllPos) T finds the repeats from earlier chunks at no lag, so L only adds a
@@ -100,7 +113,9 @@ constexpr bool kAllPos = APE_LZ4_ALLPOS != 0;
 #define APE_LZ4_NOL 1
 #endif
 #ifndef APE_LZ4_TSIZE
-#if APE_LZ4_NOL
+#if APE_LZ4_NOL && APE_LZ4_ONEBAR
+#define APE_LZ4_TSIZE 7072           // (the second info buffer takes 256 entries)
+#elif APE_LZ4_NOL
 #define APE_LZ4_TSIZE 7328
 #else
 #define APE_LZ4_TSIZE 7200
@@ -187,7 +202,7 @@ struct __attribute__((aligned(16))) EncLds {
     // 0, so that a read's dwords share one address register (ds_read2 offsets)
     uint32_t ring[kRingE / 4 + 16];
     uint16_t tab[kHSize];
-    uint2 info[64];                  // producer -> walker: chunk k, written in the second half of
+    uint2 info[kInfoBufs][64];       // producer -> walker: chunk k in [k % kInfoBufs], written in the second half of
                                      // step k, read at the start of step k + 1 (before the
                                      // producer writes chunk k + 1 after the mid barrier)
 #if !APE_LZ4_NOL
@@ -195,7 +210,8 @@ struct __attribute__((aligned(16))) EncLds {
 #endif
     uint2 q[kQ];                     // walker -> emitter: sequence records, record r in
                                      // [r % kQ]: {lit | (match length - 4) << 16, offset}
-    uint32_t qn;                     // walker -> emitter: records published
+    uint32_t qn[2];                  // walker -> emitter: records published, by step parity (the
+                                     // emitter of step s reads the count of step s - 1)
     uint8_t __attribute__((aligned(16))) stage[kStageAlloc];   // emitter: one batch's bytes
 };
 
@@ -721,7 +737,7 @@ __device__ __forceinline__ void prod_finish(EncLds &S, const Blk &B, int k, int 
     }
     // (FAST: the chunk lies inside the block, every lane hashable -- also the prologue's
     // chunk when the first step is FAST)
-    S.info[lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
+    S.info[(uint32_t)k & (kInfoBufs - 1u)][lane] = make_uint2(len | (R.bk << 8) | (trunc ? I_TRUNC : 0u) |
                                   ((FAST || R.hashable) ? I_HASHABLE : 0u),
                                      R.iy);
 }
@@ -856,7 +872,7 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     const uint32_t P = 64u * (uint32_t)k;
     O.walked = O.members = 0;
     O.m_back = O.m_len = O.an = 0;
-    O.iv = S.info[lane];
+    O.iv = S.info[(uint32_t)k & (kInfoBufs - 1u)][lane];
     O.q0 = W.q;
     O.Lf = O.iv.x & 0x7Fu;                               // forward match length
     // match_end - 2 (:680) of every lane's match, read from the ring now so that the
@@ -970,7 +986,7 @@ __device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk 
 }
 
 __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int lane,
-                                             const WalkOut &O, uint32_t &qn) {
+                                             const WalkOut &O, uint32_t &qn, int step) {
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     const uint2 iv = O.iv;
     const bool mem = lane_in(O.members);
@@ -998,7 +1014,7 @@ __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int
     if (mem) S.q[(qn + lane_rank(O.members)) & (kQ - 1u)] =
         make_uint2(((p - O.m_back) - O.an) | ((O.m_len - kMinMatch) << 16), iv.y & 0xFFFFu);
     qn += (uint32_t)__popcll(O.members);
-    if (lane == 0) S.qn = qn;
+    if (lane == 0) S.qn[step & 1] = qn;
 }
 
 // ---------------- emitter ----------------
@@ -1274,7 +1290,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             STAT(9);
             prod_measure<SMALL, F>(S, B, s + 1, lane, X6, nxt.Y, nxt.cT, nxt.jL, nxt.h, nxt.q);
             STAT(5);
-            __syncthreads();
+            if constexpr (!kOneBar) __syncthreads();
             STAT(6);
             prod_stage2_issue<SMALL, F>(S, B, s + 1, lane, nxt.q, nxt.E);
             // E(s), A(s+3), Y(s+2) x2, E(s+1) -> E(s) at 4 (A(s+3), issued half a step ago,
@@ -1339,15 +1355,15 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         // the walking loop carries no per-step predicate)
         const int s2 = nch + 1;
         __syncthreads();   // step k0
-        __syncthreads();
+        if constexpr (!kOneBar) __syncthreads();
         int s = k0 + 1;
         for (; s < s2; s++) {
             walk_chain<ACC>(S, B, s - 1, lane, W, O);
             STAT(0);
-            __syncthreads();
+            if constexpr (!kOneBar) __syncthreads();
             STAT(4);
             walk_finish<ACC>(B, s - 1, lane, W, O);
-            walk_publish(S, B, s - 1, lane, O, qn);
+            walk_publish(S, B, s - 1, lane, O, qn, s);
             STAT_ADD(11, __popcll(O.members));
             STAT(1);
             STAT_ADD(10, 3);
@@ -1356,7 +1372,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         }
         for (; s < nsteps; s++) {
             __syncthreads();
-            __syncthreads();
+            if constexpr (!kOneBar) __syncthreads();
         }
         STATS_FLUSH(g_enc_stats);
         return;
@@ -1377,8 +1393,8 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
     E.r = E.lit = E.mlm4 = E.off = E.ba = 0;
     __syncthreads();
     for (int s = k0; s < nsteps; s++) {
-        // S.qn: the walker's count as of its last publish (before the previous barrier)
-        const uint32_t avail = (uint32_t)__builtin_amdgcn_readfirstlane(S.qn) - E.qc;
+        // the walker's count as of its publish in step s - 1 (before the previous barrier)
+        const uint32_t avail = (uint32_t)__builtin_amdgcn_readfirstlane(S.qn[(s - 1) & 1]) - E.qc;
         if (E.pend == 0) {
             if (avail != 0u && (avail >= kFetchAt || s - E.last >= APE_EMIT_EVERY)) {
                 // piece L runs in the second half of step s, when the ring holds input
@@ -1393,7 +1409,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             emit_step(S, B, lane, E);
         }
         STAT(2);
-        __syncthreads();
+        if constexpr (!kOneBar) __syncthreads();
         STAT(14);
         if (E.pend == 1 || E.pend == 3) emit_step(S, B, lane, E);   // L or C
         STAT(12);
@@ -1405,7 +1421,8 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
     emit_all(S, B, lane, E);
     {
         const uint32_t rlo = B.nch > 16 ? 64u * (uint32_t)(B.nch - 16) : 0u;
-        for (uint32_t left = (uint32_t)__builtin_amdgcn_readfirstlane(S.qn) - E.qc; left;) {
+        // (counts only grow: the later of the two parities is the larger)
+        for (uint32_t left = (uint32_t)__builtin_amdgcn_readfirstlane(umax(S.qn[0], S.qn[1])) - E.qc; left;) {
             const uint32_t qc0 = E.qc;
             emit_fetch(S, B, lane, E, left, rlo);
             emit_all(S, B, lane, E);
@@ -1485,7 +1502,7 @@ lz4_encode_kernel(BlockArgs a) {
     for (int i = tid; i < (int)kScr; i += 192) S.scr[i] = 0xFFFFFFFFu;
 #endif
     for (int i = tid; i < (int)(kRingE / 16 + 4); i += 192) ((uint4 *)S.ring)[i] = make_uint4(0, 0, 0, 0);
-    if (tid == 0) S.qn = 0u;
+    if (tid == 0) S.qn[0] = S.qn[1] = 0u;
     __syncthreads();
     if (B.n < kSmall) encode_block<true, ACC>(S, B, wave, lane, &a.result[b]);
     else encode_block<false, ACC>(S, B, wave, lane, &a.result[b]);
