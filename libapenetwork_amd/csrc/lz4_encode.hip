@@ -180,14 +180,6 @@ constexpr bool kNoL = APE_LZ4_NOL != 0;
 #ifndef APE_LZ4_APF
 #define APE_LZ4_APF 1                // producer: own-bytes load A two steps ahead (else one)
 #endif
-// Own bytes through the ring (1): A loads a chunk's 64 bytes with 8 lanes (one line; the other
-// lanes repeat lane 7's address) into the ring three steps ahead of C1, and B hashes from the
-// ring -- instead of 64 lanes loading 8 bytes each at a 1-byte stride (the texture path is the
-// encoder's binding unit).  Needs APE_LZ4_APF.
-#ifndef APE_LZ4_RINGA
-#define APE_LZ4_RINGA 1
-#endif
-static_assert(!APE_LZ4_RINGA || APE_LZ4_APF, "own bytes through the ring need A two steps ahead");
 #ifndef APE_LZ4_CAPBITS
 #define APE_LZ4_CAPBITS 1            // length caps folded into the bit-index mins (v_min3)
 #endif
@@ -505,14 +497,11 @@ struct PSet {
     Part q;
 };
 
-// A(k): own bytes in[p, p+8) for the hash (0 past the block end); with APE_LZ4_RINGA chunk k's
-// 64 bytes, in[64k + 8 l, +8) on lanes l = 0..7 (lanes 8..63 repeat lane 7's address)
+// A(k): own bytes in[p, p+8) for the hash (0 past the block end)
 template <bool SMALL, bool FAST = false>
 __device__ __forceinline__ void prod_load(const Blk &B, int k, int lane, uint32_t (&X)[2]) {
-    const uint32_t pos = (FAST || k < B.nch ? 64u * (uint32_t)k : 0u) +
-                         (APE_LZ4_RINGA ? 8u * umin((uint32_t)lane, 7u) : (uint32_t)lane);
-    if (FAST || (!SMALL && 64 * k + (APE_LZ4_RINGA ? 64 : 72) <= B.n)) {   // wave-uniform: the
-                                                                            // window is inside
+    const uint32_t pos = (FAST || k < B.nch ? 64u * (uint32_t)k : 0u) + (uint32_t)lane;
+    if (FAST || (!SMALL && 64 * k + 72 <= B.n)) {   // wave-uniform: the whole window is inside
         const uint2 v = gload8(B.in + pos);
         X[0] = v.x;
         X[1] = v.y;
@@ -548,13 +537,7 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
     const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
     // (FAST: chunk k lies inside the block with room to spare, every lane is hashable)
     const bool hashable = FAST || (k < B.nch && p + 5u <= B.un);
-#if APE_LZ4_RINGA   // chunks k and k + 1 are in the ring (prod_ring three steps ahead of C1)
-    (void)X;
-    const uint2 xr = ring8(S, p);
-    h = hashk(xr.x, xr.y);
-#else
     h = hashk(X[0], X[1]);
-#endif
     cT = S.tab[h];
     jL = 0xFFFFFFFFu;
     if (!kNoL && !B.noL) {   // wave-uniform
@@ -581,21 +564,12 @@ __device__ __forceinline__ void prod_lookup(EncLds &S, const Blk &B, int k, int 
 template <bool FAST = false>
 __device__ __forceinline__ void prod_ring(EncLds &S, const Blk &B, int k, int lane,
                                           const uint32_t (&X)[2]) {
-#if APE_LZ4_RINGA   // lanes 0..7 hold the chunk's 64 bytes: one 8-byte write each
-    if ((FAST || k < B.nch) && lane < 8) {
-        const uint32_t o = (64u * (uint32_t)k + 8u * (uint32_t)lane) & (kRingE - 1);
-        *(uint2 *)((uint8_t *)S.ring + o) = make_uint2(X[0], X[1]);
-        if (((64u * (uint32_t)k) & (kRingE - 1)) == 0u)
-            *(uint2 *)((uint8_t *)S.ring + kRingE + 8u * (uint32_t)lane) = make_uint2(X[0], X[1]);
-    }
-#else
     if (FAST || k < B.nch) {
         const uint32_t p = 64u * (uint32_t)k + (uint32_t)lane;
         const uint8_t by = (uint8_t)X[0];
         ((uint8_t *)S.ring)[p & (kRingE - 1)] = by;
         if (((64u * (uint32_t)k) & (kRingE - 1)) == 0u) ((uint8_t *)S.ring)[kRingE + lane] = by;
     }
-#endif
 }
 
 // own bytes in[p-4, p+20) of chunk k from the ring (ring tail = 0 before 0)
@@ -1296,17 +1270,10 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             // s+1 and s+2) from the ring: one wave's LDS operations complete in order.  (Until
             // round 3 chunk s+3 was copied in the second half of step s, which then waited
             // for a load issued half a step earlier: -2.7 % encode time.)
-#if APE_LZ4_RINGA   // ring copy of chunk s+3 (B(s+2) hashes from chunks s+2 and s+3)
-            prod_ring<F>(S, B, s + 3, lane, cur.X);
-#else
             prod_ring<F>(S, B, s + 2, lane, cur.X);
-#endif
             uint32_t X6[6];   // C1(s+1)'s own bytes: in the ring since last step, read first
             prod_own(S, s + 1, lane, X6);
-#if APE_LZ4_RINGA
-            prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
-            prod_load<SMALL, F>(B, s + 5, lane, cur.X);   // -> the ring copy of step s + 2
-#elif APE_LZ4_APF
+#if APE_LZ4_APF
             prod_lookup<SMALL, F>(S, B, s + 2, lane, cur.X, cur.cT, cur.jL, cur.h, cur.Y);
             // A two steps ahead, into the set B(s+2) has just consumed: the block's own input
             // streams in from HBM, and one step (~1 us) did not cover it (the producer's load
@@ -1337,24 +1304,6 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             STAT(8);
         };
         if (k0 > 0) prefix_history(S, B, lane);
-#if APE_LZ4_RINGA
-        if (nch > k0) {  // prologue: rings k0..k0+2, B(k0), B(k0+1), A(k0+3), A(k0+4), C1(k0)
-            prod_load<SMALL>(B, k0, lane, P0.X);
-            prod_load<SMALL>(B, k0 + 1, lane, P1.X);
-            prod_ring(S, B, k0, lane, P0.X);
-            prod_ring(S, B, k0 + 1, lane, P1.X);
-            prod_load<SMALL>(B, k0 + 2, lane, P0.X);
-            prod_ring(S, B, k0 + 2, lane, P0.X);
-            prod_lookup<SMALL>(S, B, k0, lane, P0.X, P0.cT, P0.jL, P0.h, P0.Y);
-            prod_lookup<SMALL>(S, B, k0 + 1, lane, P1.X, P1.cT, P1.jL, P1.h, P1.Y);
-            prod_load<SMALL>(B, k0 + 3, lane, P0.X);   // the ring copies of steps k0, k0 + 1
-            prod_load<SMALL>(B, k0 + 4, lane, P1.X);
-            uint32_t X6[6];
-            prod_own(S, k0, lane, X6);
-            prod_measure<SMALL>(S, B, k0, lane, X6, P0.Y, P0.cT, P0.jL, P0.h, P0.q);
-            prod_stage2_issue<SMALL>(S, B, k0, lane, P0.q, P0.E);
-        }
-#else
         if (nch > k0) {  // prologue: A(k0), A(k0+1), B(k0), A(k0+2), B(k0+1), C1(k0)
             prod_load<SMALL>(B, k0, lane, P0.X);
             prod_load<SMALL>(B, k0 + 1, lane, P1.X);
@@ -1370,7 +1319,6 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
             prod_measure<SMALL>(S, B, k0, lane, X6, P0.Y, P0.cT, P0.jL, P0.h, P0.q);
             prod_stage2_issue<SMALL>(S, B, k0, lane, P0.q, P0.E);
         }
-#endif
         // nothing in flight at the loop entry, so the loop's counter waits depend only
         // on its own issue order (once per block)
         __builtin_amdgcn_s_waitcnt(0);
@@ -1379,8 +1327,7 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         // Y(s+2): 64(s+2)+83, E(s+1): 64(s+1)+148) run a loop without the edge paths;
         // the last few steps run the general one.
         // (APF: A(s+4), 64(s+4)+72 <= n)
-        // (RINGA: A(s+5), 64(s+5)+64 <= n)
-        constexpr int kFastEnd = APE_LZ4_RINGA ? 384 : (APE_LZ4_APF ? 328 : 264);
+        constexpr int kFastEnd = APE_LZ4_APF ? 328 : 264;
         const int nfast_abs = SMALL ? 0 : (int)umin((uint32_t)(B.n >= kFastEnd ? (B.n - kFastEnd) / 64 + 1 : 0),
                                                     (uint32_t)nsteps);
         const int nfast = nfast_abs > k0 ? k0 + ((nfast_abs - k0) & ~1) : k0;
