@@ -9,13 +9,18 @@ the bound, bound - 1, 0 and random values, through two product entry points:
     a nonzero block decodes with the oracle to the input, a capacity >= compressBound never
     fails, an empty input returns what the oracle returns;
   * APE_LZ4_compress_exact_batch_dev (greedy-exact mode): ret and bytes equal to the oracle's
-    compress_fast at the same capacity (limitedOutput) and acceleration.
+    compress_fast at the same capacity (limitedOutput) and acceleration;
+  * APE_LZ4_compress_withPrefix_batch_dev (round 6): chunks of 0 .. 64 KiB of a mixed stream with
+    0 .. 64 KiB of the stream before them as history, every block decoded by the oracle's
+    decompress_safe_usingDict with that history to the chunk.
 Canaries around every dst slot are checked per batch (nothing written outside dst[0:cap)).
 
   python3 tests/fuzz/gpu_encode_fuzz.py SECONDS [SEED]
 prints one progress line per batch and a JSON summary; exit 1 on the first mismatch."""
 import ctypes
 import json
+
+import numpy as np
 import os
 import random
 import sys
@@ -55,7 +60,7 @@ def main():
         sys.exit("no GPU")
     orc = ctypes.CDLL(os.path.join(os.path.dirname(TESTS), "oracle", "liblz4_oracle.so"))
     rng = random.Random(seed)
-    t0, nb, checked = time.time(), 0, {"chunk": 0, "exact": 0}
+    t0, nb, checked = time.time(), 0, {"chunk": 0, "exact": 0, "prefix": 0}
     while time.time() - t0 < seconds:
         srcs = [block(rng) for _ in range(1000)]
         accel = rng.choice([1, 1, 1, 2, 8])
@@ -101,6 +106,39 @@ def main():
                     fail("roundtrip", decoded=dr, **info)
             check_canaries()
             checked[mode] += len(srcs)
+        # withPrefix: chunks of one stream against the bytes before them
+        plain = b"".join(srcs[:160])[:3 << 20]
+        if len(plain) > 70000:
+            starts, lens, pres = [], [], []
+            for _ in range(400):
+                ln = rng.choice([0, 1, 13, 64, 300, 4096, 8192, 65536, rng.randrange(65537)])
+                st = rng.randrange(0, len(plain) - ln + 1)
+                pres.append(min(st, rng.choice([0, 64, 4096, 65536, rng.randrange(65537)])))
+                starts.append(st)
+                lens.append(ln)
+            dplain = torch.from_numpy(np.frombuffer(plain + bytes(64), np.uint8).copy()).cuda()
+            pcaps = [amd.compressBound(ln) for ln in lens]
+            dst, dptr, doffs = alloc_out(torch, pcaps)
+            res = ints(torch, [0] * len(starts))
+            amd.compress_prefix_batch(
+                torch.tensor([dplain.data_ptr() + st for st in starts], dtype=torch.int64, device="cuda"),
+                ints(torch, lens), ints(torch, pres), dptr, ints(torch, pcaps), res)
+            torch.cuda.synchronize()
+            rs = res.cpu().tolist()
+            for i, (st, ln, pr, r) in enumerate(zip(starts, lens, pres, rs)):
+                info = dict(mode="prefix", batch=nb, block=i, n=ln, prefix=pr, gpu=r)
+                if r <= 0 or r > pcaps[i]:
+                    if not (ln == 0 and r == 1):
+                        fail("range", **info)
+                comp = fetch(dst, doffs[i], r)
+                d = ctypes.create_string_buffer(plain[st - pr:st] + b"\0", pr + 1)
+                o = ctypes.create_string_buffer(ln + 64)
+                dr = orc.orc_decompress_safe_usingDict(ctypes.c_char_p(comp + bytes(16)), o, len(comp),
+                                                       ln, d, pr)
+                if dr != ln or o.raw[:ln] != plain[st:st + ln]:
+                    fail("prefix roundtrip", decoded=dr, **info)
+            check_canaries()
+            checked["prefix"] += len(starts)
         nb += 1
         print("batch %d: %d blocks x 2 modes, %.0f s" % (nb, checked["chunk"], time.time() - t0),
               flush=True)

@@ -311,6 +311,7 @@ static uint32_t kslot(const uint8_t *p, int key) {
     return (uint32_t)(((uint64_t)hkey(p, key) * (uint32_t)g_tsize) >> 32);
 }
 static int g_lag = 3, g_bcap = 4, g_noL = 0, g_near = 0, g_nearbits = 6, g_nearwin = 768, g_allins = 0, g_insd = 0;
+static FILE *g_seqf = NULL;   /* SEQDUMP: (lit, match length, offset) int32 triples per sequence, -1 -1 -1 per block end */
 static long model5(const uint8_t *in, int n, int key, int tmod, long *nseq)
 {
     int tab[8192], near[1024], tabold[64];
@@ -384,6 +385,7 @@ static long model5(const uint8_t *in, int n, int key, int tmod, long *nseq)
                 int lit = m - anchor;
                 out += 1 + ext(lit) + lit + 2 + ext(len - 4);
                 (*nseq)++;
+                if (g_seqf) { const int t[3] = {lit, len, m - c}; fwrite(t, 4, 3, g_seqf); }
                 p = m + len;
                 anchor = p;
                 if (!g_allins) { ins[nins] = p - 2; insc[nins++] = (p - 2) / 64 > k ? (p - 2) / 64 : k; }
@@ -391,6 +393,7 @@ static long model5(const uint8_t *in, int n, int key, int tmod, long *nseq)
         }
     }
     out += 1 + ext(n - anchor) + n - anchor;
+    if (g_seqf) { const int t[3] = {n - anchor, -1, -1}; fwrite(t, 4, 3, g_seqf); }
     free(cT); free(cL); free(ins); free(insc);
     return out;
 }
@@ -410,6 +413,16 @@ static void key_study(const uint8_t *buf, int n, int nb, const char *what)
         g_lag = 3; g_bcap = 4; g_noL = 0;
     }
     g_tsize = getenv("TSIZE") ? atoi(getenv("TSIZE")) : 7200;
+    if (getenv("SEQDUMP")) {   /* the HEAD policy's parse of these blocks -> sequences */
+        g_allins = 1; g_noL = 1; g_tsize = 7328;
+        g_seqf = fopen(getenv("SEQDUMP"), "wb");
+        long tot = 0, nseq = 0;
+        for (int b = 0; b < nb; b++) tot += model5(buf + (size_t)b * n, n, 7, 1, &nseq);
+        fclose(g_seqf);
+        g_seqf = NULL;
+        printf("%-5s HEAD policy ratio %.4f seq %.1f\n", what, (double)n * nb / tot, (double)nseq / nb);
+        exit(0);
+    }
     if (getenv("ALLINS")) {
         const int ds[] = {0, 0, 256, 1024, 4096, 16384, 1 << 20};
         const int nv = getenv("ALLINS")[0] == '2' ? 2 : 7;
