@@ -1332,6 +1332,9 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
                                                     (uint32_t)nsteps);
         const int nfast = nfast_abs > k0 ? k0 + ((nfast_abs - k0) & ~1) : k0;
         int s = k0;
+#ifdef APE_EXP_PUNROLL
+#pragma unroll APE_EXP_PUNROLL
+#endif
         for (; s < nfast; s += 2) {   // no conditional step: see pstep
             pstep(std::true_type{}, s, P0, P1);
             pstep(std::true_type{}, s + 1, P1, P0);
@@ -1357,6 +1360,9 @@ __device__ __forceinline__ void encode_block(EncLds &S, const Blk &B, int wave, 
         __syncthreads();   // step k0
         if constexpr (!kOneBar) __syncthreads();
         int s = k0 + 1;
+#ifdef APE_EXP_WUNROLL
+#pragma unroll APE_EXP_WUNROLL
+#endif
         for (; s < s2; s++) {
             walk_chain<ACC>(S, B, s - 1, lane, W, O);
             STAT(0);

@@ -63,18 +63,26 @@ def main():
         f = L.APE_LZ4_compress_batch_strided_dev
         f.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
                       C.c_void_p, C.c_int, C.c_void_p]
-        row = []
+        row, tms = [], []
         for k, d in data.items():
             import numpy as np
             src.copy_(torch.from_numpy(np.frombuffer(d, dtype=np.uint8).reshape(nb, N).copy()))
-            f(src.data_ptr(), N, sizes.data_ptr(), comp.data_ptr(), slot, None, csz.data_ptr(), nb,
-              None)
-            torch.cuda.synchronize()
+            ts = []
+            for _ in range(5):   # encode time of the 64 blocks (median of 5, HIP events)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                f(src.data_ptr(), N, sizes.data_ptr(), comp.data_ptr(), slot, None, csz.data_ptr(),
+                  nb, C.c_void_p(torch.cuda.current_stream().cuda_stream))
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            tms.append(sorted(ts)[2])
             amd.decompress_batch(comp, csz, out, dres, dst_caps=sizes)
             torch.cuda.synchronize()
             ok = bool((dres == N).all()) and bool(torch.equal(out, src))
             row.append(nb * N / int(csz.sum()) if ok else float("nan"))
-        print("%-8s" % v + "".join("%10.4f" % r for r in row), flush=True)
+        print("%-8s" % v + "".join("%10.4f" % r for r in row) +
+              "   encode ms (64 blocks): " + " ".join("%.3f" % t for t in tms), flush=True)
 
 
 if __name__ == "__main__":
