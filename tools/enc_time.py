@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """enc_time.py -- DESIGN TOOL (GPU box): median HIP-event time of compress_batch over 131072 App. C
-blocks for the library APE_LZ4_LIB names (a variant built by tools/src_variant.sh or make variant);
+blocks for the library APE_LZ4_LIB names (a variant built by tools/enc_variant.sh or make variant);
 for variants whose output is not a valid block (sensitivity builds), where tools/ab_inproc.py stops."""
 import os, sys, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
