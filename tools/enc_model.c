@@ -312,6 +312,11 @@ static uint32_t kslot(const uint8_t *p, int key) {
 }
 static int g_lag = 3, g_bcap = 4, g_noL = 0, g_near = 0, g_nearbits = 6, g_nearwin = 768, g_allins = 0, g_insd = 0;
 static FILE *g_seqf = NULL;   /* SEQDUMP: (lit, match length, offset) int32 triples per sequence, -1 -1 -1 per block end */
+/* SEQDUMP also prints, for the T gather of the HEAD policy: lanes with no candidate, a candidate
+   <= 832 bytes back (in the ring at C1) that verifies / does not, one further back that verifies /
+   does not, all lanes; distinct 64-byte lines per chunk, all lanes / near lanes on one line
+   (profiles/r6_encoder_policy_ab.txt call 16) */
+static long g_cnt[6], g_lines[3];
 static long model5(const uint8_t *in, int n, int key, int tmod, long *nseq)
 {
     int tab[8192], near[1024], tabold[64];
@@ -333,6 +338,15 @@ static long model5(const uint8_t *in, int n, int key, int tmod, long *nseq)
             uint32_t h = q + 8 <= n ? kslot(in + q, key) : 0;
             cT[q] = (q % tmod == 0) ? tab[h] : -1;
             tabold[q - r0] = tab[h];
+            {
+                const int c = cT[q];
+                g_cnt[5]++;
+                if (c < 4 || c >= q || q + 8 > n) g_cnt[0]++;
+                else {
+                    const int ok = rd32(in + c) == rd32(in + q);
+                    g_cnt[(q - c <= 832 ? 1 : 3) + !ok]++;
+                }
+            }
             cL[q] = -1;
             if (g_near == 2) {
                 /* one ds_max_rtn per lane on ((k+1) << 6 | 63 - lane) over 2^nearbits buckets,
@@ -352,6 +366,23 @@ static long model5(const uint8_t *in, int n, int key, int tmod, long *nseq)
                 const int nb = h & ((1 << g_nearbits) - 1);
                 if (g_near && near[nb] >= 0 && q - near[nb] <= g_nearwin) cL[q] = near[nb];
             } else if (!g_noL) cL[q] = scr[h & 63];
+        }
+        {   /* distinct 64-B lines of the T gather (in[T-4, T+12) per valid lane, the lane's own p line
+               otherwise): every lane, and with lanes whose candidate is <= 832 back verified from LDS */
+            long ls[2][160]; int nl[2] = {0, 0};
+            for (int q = r0; q < r1; q++) {
+                const int c = cT[q], valid = c >= 4 && c < q && q + 8 <= n;
+                for (int v = 0; v < 2; v++) {
+                    const int use = valid && !(v && q - c <= 832);
+                    const long a0 = use ? c - 4 : q, a1 = use ? c + 11 : q;
+                    for (long L = a0 >> 6; L <= a1 >> 6; L++) {
+                        int f = 0;
+                        for (int i = 0; i < nl[v]; i++) f |= ls[v][i] == L;
+                        if (!f) ls[v][nl[v]++] = L;
+                    }
+                }
+            }
+            g_lines[0] += nl[0]; g_lines[1] += nl[1]; g_lines[2]++;
         }
         if (g_near == 1)
             for (int q = r0; q < r1; q++) if (q + 8 <= n) near[kslot(in + q, key) & ((1 << g_nearbits) - 1)] = q;
@@ -421,6 +452,10 @@ static void key_study(const uint8_t *buf, int n, int nb, const char *what)
         fclose(g_seqf);
         g_seqf = NULL;
         printf("%-5s HEAD policy ratio %.4f seq %.1f\n", what, (double)n * nb / tot, (double)nseq / nb);
+        printf("lanes: none %.3f  near ok %.3f bad %.3f  far ok %.3f bad %.3f\n", (double)g_cnt[0] / g_cnt[5],
+               (double)g_cnt[1] / g_cnt[5], (double)g_cnt[2] / g_cnt[5], (double)g_cnt[3] / g_cnt[5],
+               (double)g_cnt[4] / g_cnt[5]);
+        printf("gather lines/chunk: all %.2f  far-only %.2f\n", (double)g_lines[0] / g_lines[2], (double)g_lines[1] / g_lines[2]);
         exit(0);
     }
     if (getenv("ALLINS")) {
