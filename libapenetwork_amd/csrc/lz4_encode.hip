@@ -595,8 +595,8 @@ __device__ __forceinline__ bool stage2_group(const Part &R, int lane, uint32_t f
     const uint32_t r = R.rank - first, i16 = 16u * ((uint32_t)lane & 3u);
     const bool push = lane_in(R.smask) && r < kGroups;
     const int tgt = (int)((push ? 4u * r : ((uint32_t)lane | 1u)) << 2);
-    cb = dpp<0x00>(0u, (uint32_t)__builtin_amdgcn_ds_permute(tgt, (int)(R.c + R.base))) + i16;
-    eo = dpp<0x00>(0u, (uint32_t)__builtin_amdgcn_ds_permute(tgt, (int)(p + R.base))) + i16;
+    cb = dpp_z<0x00>((uint32_t)__builtin_amdgcn_ds_permute(tgt, (int)(R.c + R.base))) + i16;
+    eo = dpp_z<0x00>((uint32_t)__builtin_amdgcn_ds_permute(tgt, (int)(p + R.base))) + i16;
     return first + ((uint32_t)lane >> 2) < R.ntr;
 }
 
@@ -683,7 +683,7 @@ __device__ __forceinline__ void prod_measure(EncLds &S, const Blk &B, int k, int
         // match from p is one byte longer than lane i + 1's (and lim one larger): only the
         // run's last lane is measured
         const uint32_t key = (R.c - (uint32_t)lane) + (R.base << 24);
-        const uint32_t keyn = dpp<kDppWaveShl1>(0u, key);   // lane 63: 0, never a key
+        const uint32_t keyn = dpp_z<kDppWaveShl1>(key);   // lane 63: 0, never a key
         R.smask = R.tmask & ~((R.tmask >> 1) & wave_ballot(key == keyn));
     }
 #else

@@ -65,6 +65,12 @@ template <int CTRL, int ROW_MASK = 0xF>
 __device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW_MASK, 0xF, false);
 }
+// ... with every row and bank enabled and bound_ctrl set: a lane whose source is outside
+// reads 0, and no `old` register is needed (no v_mov 0 before the move)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_z(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
 constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114,
               kDppRowShr8 = 0x118, kDppBcast15 = 0x142, kDppBcast31 = 0x143,
               kDppWaveShr1 = 0x138, kDppWaveShl1 = 0x130;
