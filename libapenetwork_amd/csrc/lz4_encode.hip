@@ -835,13 +835,25 @@ struct WalkOut {
     uint32_t q0, Lf;              // walk start; forward match length per lane
     uint2 e2v;                    // in[e2, e2 + 8), e2 = match_end - 2 (read before the walk)
     uint32_t e2h;                 // its hash
+    uint32_t pmv, pe;             // kWalkPm: per member lane, the end of the match before it
+                                  // (relative to the chunk start); the last match end (relative)
 };
+
+// The walker's catch-up limits from the hop chain itself (1): the chain writes each member's
+// previous match end into its lane (v_writelane) as it finds it, instead of a wave-wide max
+// scan over the member ends afterwards (with kAllPos and no acceleration only: the walked set,
+// which needs the limit on every lane, is not used then).  Same bytes, -0.4..-0.5 % encode
+// time (profiles/r6_encoder_policy_ab.txt call 21)
+#ifndef APE_LZ4_WPM
+#define APE_LZ4_WPM 1
+#endif
+constexpr bool kWalkPm = APE_LZ4_WPM != 0 && kAllPos;
 
 // The walker's hop chain from walk position rel (< 64): shift, find-first, add, mark,
 // v_readlane, compare, branch -- 9 scalar-unit instructions per member (the compiler's loop
 // took 13).  nxt (per lane) = the walk position after the lane's match; leaves with rel >= 64
 // (64: no match lane left), j = the last member, its bit set in M.
-__device__ __forceinline__ void hop_chain(uint64_t Hm, uint32_t nxt, uint32_t &rel, uint64_t &M,
+[[maybe_unused]] __device__ __forceinline__ void hop_chain(uint64_t Hm, uint32_t nxt, uint32_t &rel, uint64_t &M,
                                           uint32_t &j) {
     uint64_t t;
     asm volatile(
@@ -863,6 +875,39 @@ __device__ __forceinline__ void hop_chain(uint64_t Hm, uint32_t nxt, uint32_t &r
         : [hm] "s"(Hm), [nxt] "v"(nxt)
         : "scc");
 }
+// ... also writing pe (the previous match end) into lane j of pmv for each member j, pe then
+// the member's end (12 instructions per member).  The lane select goes through m0 (a VALU
+// instruction reads one SGPR on gfx9); nothing else in this kernel uses m0 (LDS instructions
+// do not on gfx950; tests/test_product_abi.py::test_encoder_m0_only_in_hop_chain checks the ISA)
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // (m0 declared clobbered: see above)
+__device__ __forceinline__ void hop_chain_pm(uint64_t Hm, uint32_t nxt, uint32_t &rel, uint64_t &M,
+                                             uint32_t &j, uint32_t &pe, uint32_t &pmv) {
+    uint64_t t;
+    asm volatile(
+        "1:\n\t"
+        "s_lshr_b64 %[t], %[hm], %[rel]\n\t"
+        "s_cmp_eq_u64 %[t], 0\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "s_ff1_i32_b64 %[j], %[t]\n\t"
+        "s_add_u32 %[j], %[j], %[rel]\n\t"
+        "s_bitset1_b64 %[m], %[j]\n\t"
+        "s_mov_b32 m0, %[j]\n\t"   // (one SGPR operand per VALU instruction: the lane in m0)
+        "v_writelane_b32 %[pmv], %[pe], m0\n\t"
+        "v_readlane_b32 %[rel], %[nxt], %[j]\n\t"
+        "s_mov_b32 %[pe], %[rel]\n\t"
+        "s_cmp_lt_u32 %[rel], 64\n\t"
+        "s_cbranch_scc1 1b\n\t"
+        "s_branch 3f\n"
+        "2:\n\t"
+        "s_mov_b32 %[rel], 64\n"
+        "3:"
+        : [rel] "+s"(rel), [m] "+s"(M), [j] "+s"(j), [t] "=&s"(t), [pe] "+s"(pe), [pmv] "+v"(pmv)
+        : [hm] "s"(Hm), [nxt] "v"(nxt)
+        : "scc", "m0");
+}
+#pragma clang diagnostic pop
 
 // First half: the hop chain only (the latency-bound part); second half, before the
 // inserts: the lane-parallel catch-up limits, walked set and anchor (walk_finish).
@@ -874,6 +919,7 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
     O.m_back = O.m_len = O.an = 0;
     O.iv = S.info[(uint32_t)k & (kInfoBufs - 1u)][lane];
     O.q0 = W.q;
+    O.pe = W.anchor - P;                                 // (kWalkPm; u32 wrap below P)
     O.Lf = O.iv.x & 0x7Fu;                               // forward match length
     // match_end - 2 (:680) of every lane's match, read from the ring now so that the
     // second half's hash needs no LDS round trip (the ring holds chunks k - 13 .. k + 2,
@@ -891,15 +937,18 @@ __device__ __forceinline__ void walk_chain(const EncLds &S, const Blk &B, int k,
         // lane's match, +256 marking a match the producer could not finish.
         const uint32_t nxt = (uint32_t)lane + (iv.x & 0x7Fu) + ((iv.x & 0x80u) << 1);
         uint32_t j = 0;
-        hop_chain(Hm, nxt, rel, M, j);
+        if constexpr (kWalkPm) hop_chain_pm(Hm, nxt, rel, M, j, O.pe, O.pmv);
+        else hop_chain(Hm, nxt, rel, M, j);
         while (__builtin_expect(rel >= 256u, 0)) {   // unfinished (rare): the wave extends it
             const uint32_t me = P + j;
             const uint32_t cm = me - (lane_val(iv.y, (int)j) & 0xFFFFu);
             const uint32_t Le = extend_match(B, me, cm, rel - 256u - j, lane);
             if ((uint32_t)lane == j) O.Lf = Le;
             rel = j + Le;
+            O.pe = rel;
             if (rel >= 64u) break;
-            hop_chain(Hm, nxt, rel, M, j);
+            if constexpr (kWalkPm) hop_chain_pm(Hm, nxt, rel, M, j, O.pe, O.pmv);
+            else hop_chain(Hm, nxt, rel, M, j);
         }
         O.members = M;
         W.q = P + rel;
@@ -950,9 +999,16 @@ __device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk 
     const uint32_t anchor0 = W.anchor;
     const bool mem = lane_in(O.members);
     const uint32_t p = P + (uint32_t)lane;
-    const uint32_t end = mem ? p + O.Lf : 0u;
-    const uint32_t imax = wave_incl_max(end);
-    const uint32_t pm = umax(wave_shr1(imax, 0u), anchor0);
+    uint32_t pm, lastend;
+    if constexpr (kWalkPm && !ACC) {   // (member lanes only: the others' limit is unused)
+        pm = P + O.pmv;
+        lastend = P + O.pe;
+    } else {
+        const uint32_t end = mem ? p + O.Lf : 0u;
+        const uint32_t imax = wave_incl_max(end);
+        pm = umax(wave_shr1(imax, 0u), anchor0);
+        lastend = umax(anchor0, lane_val(imax, 63));
+    }
     uint32_t bk = umin((O.iv.x >> 8) & 7u, p - pm);
     if (ACC) {
         // acceleration probes every stride-th position, so a match found at a probe often
@@ -982,7 +1038,7 @@ __device__ __forceinline__ void walk_finish(const Blk &B, int k, int lane, Walk 
         w = w && probed(p - pm, pm == anchor0, R, B.stride);
     }
     O.walked = wave_ballot(w);
-    W.anchor = umax(anchor0, lane_val(imax, 63));
+    W.anchor = lastend;
 }
 
 __device__ __forceinline__ void walk_publish(EncLds &S, const Blk &B, int k, int lane,

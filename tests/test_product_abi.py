@@ -310,3 +310,27 @@ def test_c_caller_links_like_ape_socket(product, golden, tmp_path):
         assert frames == want, kat["content"]
         n = len(msgs)
         assert out[4 + fb:4 + fb + n] == msgs and out[4 + fb + n:] == msgs
+
+
+def test_encoder_m0_only_in_hop_chain(tmp_path):
+    """The walker's hop chain (lz4_encode.hip hop_chain_pm) passes its lane select through m0
+    and declares m0 clobbered, which clang accepts for a reserved register without preserving
+    it: the kernel is correct only while nothing else in it keeps a value in m0.  Compile the
+    encoder as the Makefile does and check every m0 reference in the ISA is the chain's own."""
+    import shutil
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc absent")
+    csrc = os.path.join(ROOT, "libapenetwork_amd", "csrc")
+    out = tmp_path / "enc.s"
+    subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics",
+                    "-mllvm", "-amdgpu-sched-strategy=max-ilp", "-I" + csrc,
+                    "-I" + os.path.join(ROOT, "include"), "-S", "--cuda-device-only",
+                    os.path.join(csrc, "lz4_encode.hip"), "-o", str(out)],
+                   check=True, capture_output=True)
+    uses = [ln.split(";")[0].strip() for ln in out.read_text().splitlines()
+            if "m0" in ln.split(";")[0] and not ln.lstrip().startswith((".", ";"))]
+    assert uses, "the hop chain's m0 moves are gone: update this test with the asm"
+    bad = [u for u in uses if not (u.startswith("s_mov_b32 m0,") or
+                                   (u.startswith("v_writelane_b32") and u.endswith(", m0")))]
+    assert not bad, bad
